@@ -1,0 +1,140 @@
+/*
+ * videoprism_hip.h — C-ABI of the MI355X (gfx950) VideoPrism video-encoder library
+ * (libvideoprism_hip.so).
+ *
+ * The reference (tmoroney/videoprism-mlx) has no native FFI: its drop-in surface is the
+ * Python API `models.get_model(name, fprop_dtype=...)` + `model.apply(variables, inputs,
+ * train=False, return_intermediate=..., frame_paddings=...)` (videoprism/models.py:268-303,
+ * videoprism/encoders.py:411-580) and `models_mlx.load_video_encoder(name, weights_path)`
+ * (videoprism/models_mlx.py:146-210).  This header is the boundary those Python entry
+ * points (videoprism-mlx_amd/videoprism/) bind through ctypes; any other host language
+ * binds the same symbols.
+ *
+ * Conventions
+ *  - Every function returns an int status (VP_OK == 0).  On failure a thread-local
+ *    message is available from vp_last_error().  VP_EINVAL carries the same messages the
+ *    reference raises as ValueError/AssertionError (e.g. encoders.py:86-90).
+ *  - Plain pointers and sizes only.  Device pointers are HIP device memory of the handle's
+ *    device; `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *  - Parameters are passed once, as HOST fp32 arrays in the reference's own Flax layout
+ *    and names (scanned layers, leading L axis), and are repacked by the library into
+ *    kernel-ready device buffers owned by the handle.
+ *  - vp_forward never allocates, never synchronises: all activations live in the caller's
+ *    workspace (size from vp_workspace_bytes); the call is asynchronous on `stream` and
+ *    can be captured into a hipGraph.
+ *  - A handle is bound to one device and is not thread-safe.
+ */
+#ifndef VIDEOPRISM_HIP_H_
+#define VIDEOPRISM_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VP_ABI_VERSION 1
+
+typedef struct vp_handle vp_handle;
+
+enum vp_status {
+  VP_OK = 0,
+  VP_EINVAL = 1,   /* bad argument / shape (reference ValueError / assert) */
+  VP_ENOMEM = 2,   /* device allocation failed */
+  VP_EHIP = 3,     /* HIP runtime error */
+  VP_ESTATE = 4,   /* handle not finalized / parameter missing */
+  VP_ENOTSUP = 5,  /* valid for the reference but outside this library's kernels */
+};
+
+enum vp_dtype { VP_F32 = 0, VP_BF16 = 1 };
+
+/* FactorizedEncoder hyper-parameters: models.py:83-104 CONFIGS / encoders.py:399-408. */
+typedef struct vp_config {
+  int32_t patch_size;          /* 18 */
+  int32_t pos_emb_t;           /* pos_emb_shape[0]: 16 (Base) / 8 (Large) */
+  int32_t pos_emb_h;           /* pos_emb_shape[1]: 16 */
+  int32_t pos_emb_w;           /* pos_emb_shape[2]: 16 */
+  int32_t model_dim;           /* 768 / 1024 */
+  int32_t num_spatial_layers;  /* 12 / 24 */
+  int32_t num_temporal_layers; /* 4 */
+  int32_t num_heads;           /* 12 / 16 (dim_per_head must be 64) */
+  int32_t mlp_dim;             /* 3072 / 4096 */
+  float atten_logit_cap;       /* 50.0 */
+  int32_t fprop_dtype;         /* VP_F32 (reference default) or VP_BF16 (get_model(fprop_dtype=bf16)) */
+} vp_config;
+
+/* Last error message of the calling thread ("" if none). */
+const char* vp_last_error(void);
+int vp_abi_version(void);
+
+/* Replaces models.get_model(...) (models.py:268-303): binds a config to a device. */
+int vp_create(const vp_config* cfg, int device, vp_handle** out);
+int vp_destroy(vp_handle* h);
+
+/* One parameter leaf, by its Flax path under 'params' ('/'-joined, utils.py:84-105), e.g.
+ *   "patch_projection/linear/kernel"                                    [P*P*3, D]
+ *   "spatial_encoder/transformers_stack/x_layers/self_attention/query/w" [L, D, N, H]
+ * host_data: fp32, C-contiguous.  Shapes are validated against the config. */
+int vp_set_param(vp_handle* h, const char* name, const float* host_data, const int64_t* shape,
+                 int ndim);
+/* Number of leaves the config expects (40 for a scanned FactorizedEncoder,
+ * encoders_test.py:170) and the i-th leaf's name. */
+int vp_param_count(const vp_handle* h, int* count);
+int vp_param_name(const vp_handle* h, int index, const char** name);
+/* Validates that every leaf was set and uploads the packed weights (one-off). */
+int vp_finalize(vp_handle* h);
+
+/* Workspace needed by vp_forward for inputs [B, T, H, W, 3]. */
+int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W,
+                       size_t* bytes);
+
+/* Replaces FactorizedEncoder.__call__ (encoders.py:411-456) / model.apply(..., train=False).
+ *   video          device [B, T, H, W, 3], in_dtype VP_F32 or VP_BF16, values as given
+ *   frame_paddings device [B, T] fp32 (1 = padded frame) or NULL (encoders.py:440-447)
+ *   out            device [B, T*N, D] embeddings in out_dtype (token = t*N + n, :570-572)
+ *   spatial_out    device [B, T*N, D] 'spatial_features' in out_dtype, or NULL (:574-578)
+ */
+int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
+               int64_t W, const float* frame_paddings, void* out, int out_dtype,
+               void* spatial_out, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------- op-level entry points (kernel parity tests, benches) ---------------- */
+
+/* C[M,N] = A[M,K].W[N,K]^T + bias with epilogue:
+ *   0 store (out dtype = precision), 1 GELU(erf) [* (1-rowpad)], 2 out_f32 = resid + (.)*(1-rowpad),
+ *   3 out_f32 = (.) + pos[m % pos_rows].   precision VP_BF16: A,W bf16; VP_F32: A,W fp32.
+ * Replaces layers.py:273-313 (Dense) and :433-499 (einsum projections). */
+int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const void* W, int64_t ldw,
+               int64_t M, int64_t N, int64_t K, void* out, int64_t ldo, const float* bias,
+               const float* resid, int64_t ldr, const float* pos, int64_t pos_rows,
+               const float* rowpad, void* stream);
+
+/* Capped attention over rows qkv[num_seq*S, 3*heads*64] = [q|k|v] (q pre-scaled), writing
+ * o[num_seq*S, heads*64].  Replaces DotProductAttention._dot_atten (layers.py:601-661).
+ * precision VP_BF16 (S == 256 or S <= 16) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL. */
+int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
+                    int64_t heads, float cap, const float* key_pad, void* stream);
+
+/* LayerNorm (layers.py:208-270) of fp32 rows with gamma = 1 + scale; optional row permutation
+ * (0 none, 1 (b t n)->(b n t), 2 (b n t)->(b t n)) and fp32 add[t][D] by output t. */
+int vp_op_layernorm(const float* x, int64_t rows, int64_t D, const float* gamma, const float* beta,
+                    void* out, int out_dtype, int perm, int64_t T, int64_t Nsp, const float* add,
+                    void* stream);
+
+/* _image_to_patch (encoders.py:70-104): video [BT,H,W,C] -> patches [BT*(H/P)*(W/P), kpad]
+ * with features in (p, q, c) order and zero padding from P*P*C to kpad. */
+int vp_op_patchify(const void* video, int in_dtype, void* patches, int out_dtype, int64_t BT,
+                   int64_t H, int64_t W, int64_t C, int64_t P, int64_t kpad, void* stream);
+
+/* Build-defined pooled clip embedding used by the multi-GPU gather (the video-only encoder
+ * has no pooler in the reference): out[b] = l2norm(mean_l emb[b, l, :]) in fp32, with the
+ * reference's _l2_normalize (encoders.py:50-67, eps 1e-12). */
+int vp_op_pool_l2(const void* emb, int dtype, int64_t B, int64_t L, int64_t D, float* out,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VIDEOPRISM_HIP_H_ */

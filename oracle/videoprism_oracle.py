@@ -1,0 +1,350 @@
+"""CPU restatement of the VideoPrism FactorizedEncoder forward — TEST INFRASTRUCTURE ONLY.
+
+This module is the parity checker for the MI355X HIP path.  Only `tests/`,
+`__graft_entry__.smoke()` and the `cpu_baseline` leg of `bench.py` may import it;
+the product package (`videoprism-mlx_amd/videoprism`) never does, and the product
+path fails loudly when its HIP library is missing instead of falling back here.
+
+It restates, in plain NumPy (fp64 by default, fp32 on request, optional bf16
+rounding emulation), the Flax reference at /root/reference/videoprism:
+
+  * layers.py:31            gelu (exact erf)
+  * layers.py:39-179        mask helpers (padding mask, -0.7*finfo.max fill)
+  * layers.py:208-270       LayerNorm (biased var, eps 1e-6, scale+1, bias)
+  * layers.py:273-313       FeedForward (Dense + activation)
+  * layers.py:316-430       TransformerFeedForward (pre-LN, GELU, padding zeroing, residual)
+  * layers.py:433-499       AttentionProjection (w[D,N,H]; q/k/v and 'post' einsums)
+  * layers.py:530-746       DotProductAttention (q *= dh^-0.5, tanh cap, fp32 softmax)
+  * layers.py:749-872       Transformer (pre-LN block)
+  * layers.py:940-1041      StackedTransformer (scanned params, leading L axis)
+  * encoders.py:70-104      _image_to_patch ('(m p)(n q) c -> (m n)(p q c)')
+  * encoders.py:107-165     _interpolate_emb_1d/2d (jax.image.resize 'bilinear')
+  * encoders.py:269-307     TrainablePositionalEmbedding (slice of emb_var)
+  * encoders.py:310-388     VisionTransformer
+  * encoders.py:391-580     FactorizedEncoder.__call__ / encode_with_patches
+
+PARITY UNPINNED: the reference's own tests pin only shapes and parameter-leaf
+counts (encoders_test.py:170, models_test.py:52); JAX/Flax are not installed in
+this container (ModuleNotFoundError, not a permission denial), no checkpoint is
+available offline, and the reference ships no golden vectors for this path.  The
+restatement is therefore pinned only by those structural facts, by a second
+independent restatement (torch-CPU, tests/test_oracle.py) and by the golden
+fixtures it generated itself (tests/golden/, script tests/golden/make_golden.py).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+from scipy.special import erf as _erf
+
+F32_MAX = float(np.finfo(np.float32).max)
+
+
+# --------------------------------------------------------------------------- #
+# numeric helpers
+# --------------------------------------------------------------------------- #
+def round_bf16(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even to bfloat16, returned as float32 (emulation)."""
+    a = np.ascontiguousarray(x, dtype=np.float32)
+    u = a.view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return (u.astype(np.uint32) << 16).view(np.float32).reshape(a.shape)
+
+
+class Numerics:
+    """Where the Flax graph holds tensors in `fprop_dtype` (layers.py:182-205).
+
+    mode 'f64'  : everything float64 (mathematical reference)
+    mode 'f32'  : everything float32 (Flax fprop_dtype=float32)
+    mode 'bf16' : float32 arithmetic, activations/params rounded to bf16 at the
+                  points where Flax-bf16 stores bf16 (models.py:301-302); softmax
+                  stays fp32 (layers.py:650-654).
+    """
+
+    def __init__(self, mode: str = "f64"):
+        assert mode in ("f64", "f32", "bf16"), mode
+        self.mode = mode
+        self.dt = np.float64 if mode == "f64" else np.float32
+
+    def act(self, x):
+        x = np.asarray(x, dtype=self.dt)
+        return round_bf16(x) if self.mode == "bf16" else x
+
+    def param(self, p):
+        return self.act(p)
+
+
+# --------------------------------------------------------------------------- #
+# layers.py
+# --------------------------------------------------------------------------- #
+def gelu(x):
+    """layers.py:31 — jax.nn.gelu(approximate=False) = 0.5 x (1 + erf(x/sqrt 2))."""
+    return 0.5 * x * (1.0 + _erf(x / np.sqrt(2.0)))
+
+
+def layer_norm(x, scale, bias, nm: Numerics, eps: float = 1e-6):
+    """layers.py:208-270 (direct_scale=False, reductions_in_fp32=False)."""
+    mean = nm.act(np.mean(x, axis=-1, keepdims=True))
+    xc = nm.act(x - mean)
+    var = nm.act(np.mean(nm.act(xc * xc), axis=-1, keepdims=True))
+    normed = nm.act(xc * nm.act(1.0 / np.sqrt(var + eps)))
+    normed = nm.act(normed * nm.act(nm.param(scale) + 1.0))
+    return nm.act(normed + nm.param(bias))
+
+
+def dense(x, kernel, bias, nm: Numerics):
+    """layers.py:273-313 — nn.Dense(x @ kernel + bias), params cast to fprop dtype."""
+    y = nm.act(np.matmul(x, nm.param(kernel)))
+    return nm.act(y + nm.param(bias))
+
+
+def attention_projection_in(x, w, b, nm: Numerics):
+    """layers.py:455-499, is_output_projection=False: '...D,DNH->...NH' + b[N,H]."""
+    d, n, h = w.shape
+    y = nm.act(np.matmul(x, nm.param(w).reshape(d, n * h)))
+    y = y.reshape(*x.shape[:-1], n, h)
+    return nm.act(y + nm.param(b))
+
+
+def attention_projection_out(enc, w, b, nm: Numerics):
+    """layers.py:455-499, is_output_projection=True: '...NH,DNH->...D' + b[D]."""
+    d, n, h = w.shape
+    flat = enc.reshape(*enc.shape[:-2], n * h)
+    y = nm.act(np.matmul(flat, nm.param(w).reshape(d, n * h).T))
+    return nm.act(y + nm.param(b))
+
+
+def padding_mask(paddings):
+    """layers.py:75-89 — paddings[:,None,None,:] * (-0.7*finfo.max); 0 means keep."""
+    return paddings[:, None, None, :].astype(np.float64) * (-0.7 * F32_MAX)
+
+
+def apply_mask_to_logits(logits, mask):
+    """layers.py:51-72 — where(mask >= 0.5*min, logits, min), min = -0.7*f32max."""
+    min_value = -0.7 * F32_MAX
+    return np.where(mask >= 0.5 * min_value, logits, min_value)
+
+
+def softmax(x):
+    """jax.nn.softmax over the last axis (max-subtracted)."""
+    m = np.max(x, axis=-1, keepdims=True)
+    e = np.exp(x - m)
+    return e / np.sum(e, axis=-1, keepdims=True)
+
+
+def dot_atten(q, k, v, mask, nm: Numerics, cap: float, dim_per_head: int):
+    """layers.py:601-661 with _scale_query :569-584 and _cap_logits :586-594.
+
+    q,k,v: [B, S, N, H]; mask: [B|1, 1, 1, S] (or None for all-valid).
+    """
+    q = nm.act(q * nm.act(dim_per_head ** -0.5))          # per_dim_scale disabled
+    qt = np.transpose(q, (0, 2, 1, 3))                      # B N T H
+    kt = np.transpose(k, (0, 2, 3, 1))                      # B N H S
+    logits = nm.act(np.matmul(qt, kt))                      # 'BTNH,BSNH->BNTS'
+    if cap and cap > 0.0:
+        capv = nm.act(cap)
+        logits = nm.act(capv * nm.act(np.tanh(nm.act(logits / capv))))
+    sm_dt = np.float64 if nm.mode == "f64" else np.float32  # softmax always >= fp32
+    logits = logits.astype(sm_dt)
+    if mask is not None:
+        logits = apply_mask_to_logits(logits, mask).astype(sm_dt)
+    probs = nm.act(softmax(logits))
+    vt = np.transpose(v, (0, 2, 1, 3))                      # B N S H
+    enc = nm.act(np.matmul(probs, vt))                      # B N T H
+    return np.transpose(enc, (0, 2, 1, 3))                  # B T N H
+
+
+def transformer_layer(x, p, paddings, mask, nm: Numerics, num_heads: int, cap: float):
+    """layers.py:796-872 (norm_policy='pre', GELU, per-dim-scale off) for one layer.
+
+    `p` is the per-layer slice of the scanned 'x_layers' subtree.
+    """
+    d = x.shape[-1]
+    h = layer_norm(x, p["layer_norm"]["scale"], p["layer_norm"]["bias"], nm)
+    sa = p["self_attention"]
+    q = attention_projection_in(h, sa["query"]["w"], sa["query"]["b"], nm)
+    k = attention_projection_in(h, sa["key"]["w"], sa["key"]["b"], nm)
+    v = attention_projection_in(h, sa["value"]["w"], sa["value"]["b"], nm)
+    enc = dot_atten(q, k, v, mask, nm, cap, d // num_heads)
+    att = attention_projection_out(enc, sa["post"]["w"], sa["post"]["b"], nm)
+    x = nm.act(att + x)                                     # :855
+    # TransformerFeedForward layers.py:370-430
+    ff = p["ff_layer"]
+    y = layer_norm(x, ff["layer_norm"]["scale"], ff["layer_norm"]["bias"], nm)
+    a = nm.act(gelu(dense(y, ff["ffn_layer1"]["linear"]["kernel"],
+                          ff["ffn_layer1"]["linear"]["bias"], nm)))
+    pad = None if paddings is None else nm.act(1.0 - paddings[..., None])
+    if pad is not None:
+        a = nm.act(a * pad)
+    o = dense(a, ff["ffn_layer2"]["linear"]["kernel"], ff["ffn_layer2"]["linear"]["bias"], nm)
+    if pad is not None:
+        o = nm.act(o * pad)
+    return nm.act(x + o)
+
+
+def _layer_slice(tree, i):
+    if isinstance(tree, dict):
+        return {k: _layer_slice(v, i) for k, v in tree.items()}
+    return tree[i]
+
+
+def stacked_transformer(x, paddings, stack, nm: Numerics, num_layers: int,
+                        num_heads: int, cap: float):
+    """layers.py:990-1041 + Repeat(scan) :875-937 (params stacked on axis 0)."""
+    if paddings is None:
+        paddings = np.zeros(x.shape[:-1])
+    mask = padding_mask(paddings)
+    if not np.any(paddings):
+        mask = None                                         # exact no-op (mask == 0)
+    xl = stack["x_layers"]
+    for i in range(num_layers):
+        x = transformer_layer(x, _layer_slice(xl, i), paddings, mask, nm, num_heads, cap)
+    return x
+
+
+# --------------------------------------------------------------------------- #
+# encoders.py
+# --------------------------------------------------------------------------- #
+def image_to_patch(inputs, patch_size: int):
+    """encoders.py:70-104 — '... (m p)(n q) c -> ... (m n)(p q c)'."""
+    if inputs.ndim < 4:
+        raise ValueError(f"Image should be formatted as 4D [B, H, W, C], Shape: {inputs.shape}")
+    h, w, c = inputs.shape[-3:]
+    if h % patch_size or w % patch_size:
+        raise ValueError(f"Image height ({h}) and width ({w}) should be multiples "
+                         f"of patch_size ({patch_size}).")
+    m, n = h // patch_size, w // patch_size
+    lead = inputs.shape[:-3]
+    x = inputs.reshape(*lead, m, patch_size, n, patch_size, c)
+    nl = len(lead)
+    perm = list(range(nl)) + [nl, nl + 2, nl + 1, nl + 3, nl + 4]
+    x = np.transpose(x, perm)
+    return x.reshape(*lead, m * n, patch_size * patch_size * c)
+
+
+def _resize_weights(in_size: int, out_size: int) -> np.ndarray:
+    """jax.image.resize(method='bilinear', antialias=True) 1-D weight matrix.
+
+    Restates jax/_src/image/scale.py `compute_weight_mat` (jax version unpinned by
+    requirements.txt:5): triangle kernel, half-pixel centres, kernel widened by
+    1/scale when downsampling, columns normalised, samples outside the input
+    range zeroed.  Upsampling reduces to half-pixel linear with edge clamp, as
+    restated independently at encoders_mlx.py:104-137.  Returns W [in, out].
+    """
+    scale = out_size / in_size
+    inv_scale = 1.0 / scale
+    kernel_scale = max(inv_scale, 1.0)
+    sample_f = (np.arange(out_size) + 0.5) * inv_scale - 0.5
+    x = np.abs(sample_f[None, :] - np.arange(in_size)[:, None]) / kernel_scale
+    w = np.maximum(0.0, 1.0 - x)
+    tot = np.sum(w, axis=0, keepdims=True)
+    w = np.where(np.abs(tot) > 1000.0 * float(np.finfo(np.float32).eps),
+                 w / np.where(tot != 0, tot, 1), 0.0)
+    inside = (sample_f >= -0.5) & (sample_f <= in_size - 0.5)
+    return np.where(inside[None, :], w, 0.0)
+
+
+def interpolate_emb_1d(emb, target_len: int):
+    """encoders.py:107-130 — emb [1, N, D] -> [1, target_len, D]."""
+    if emb.ndim > 3 or emb.shape[0] != 1:
+        raise ValueError("The shape of the embedding should be (1, N, D)")
+    wt = _resize_weights(emb.shape[1], target_len)          # [N, T']
+    return np.einsum("nd,nt->td", emb[0], wt)[None]
+
+
+def interpolate_emb_2d(emb, source_shape, target_shape):
+    """encoders.py:133-165 — emb [1, H1*W1, D] -> [1, H2*W2, D] (separable bilinear)."""
+    if emb.ndim > 3 or emb.shape[0] != 1:
+        raise ValueError("The shape of the embedding should be (1, H * W, D)")
+    if emb.shape[-2] != source_shape[0] * source_shape[1]:
+        raise ValueError("The shape of the embedding does NOT match input specs.")
+    d = emb.shape[-1]
+    e = emb[0].reshape(source_shape[0], source_shape[1], d)
+    wh = _resize_weights(source_shape[0], target_shape[0])
+    ww = _resize_weights(source_shape[1], target_shape[1])
+    out = np.einsum("hwd,hi,wj->ijd", e, wh, ww)
+    return out.reshape(1, target_shape[0] * target_shape[1], d)
+
+
+def _contains(collection, key):
+    """encoders.py:36-47."""
+    return collection if isinstance(collection, bool) else key in collection
+
+
+def factorized_encoder(params, inputs, cfg: dict, mode: str = "f64",
+                       frame_paddings=None, return_intermediate=False):
+    """encoders.py:411-580 — FactorizedEncoder.__call__ + encode_with_patches.
+
+    params: the Flax tree *under* 'params' (scanned layout).  cfg: the CONFIGS
+    entry (models.py:83-104).  Returns (embeddings [B, T*N, D], outputs dict).
+    """
+    nm = Numerics(mode)
+    P = cfg["patch_size"]
+    D = cfg["model_dim"]
+    heads = cfg["num_heads"]
+    cap = cfg.get("atten_logit_cap", 0.0)
+    b, t, h, w, c = inputs.shape
+    assert h == w                                           # :435
+    x = nm.act(np.asarray(inputs).reshape(b * t, h, w, c))
+    patches = image_to_patch(x, P)                          # [BT, N, P*P*C]
+    patches_paddings = None
+    if frame_paddings is not None:
+        frame_paddings = np.asarray(frame_paddings, dtype=np.float64)
+        assert frame_paddings.shape == (b, t)
+        patches_paddings = np.repeat(frame_paddings.reshape(b * t)[:, None],
+                                     patches.shape[1], axis=-1)
+
+    pp = params["patch_projection"]["linear"]
+    feats = dense(patches, pp["kernel"], pp["bias"], nm)    # :488-494
+    sp_shape = tuple(cfg["pos_emb_shape"][-2:])
+    sp_len = int(np.prod(sp_shape))
+    sp_emb = np.asarray(params["spatial_pos_emb"]["emb_var"], dtype=np.float64)[:sp_len][None]
+    grid = (h // P, w // P)
+    if sp_shape != grid:
+        sp_emb = interpolate_emb_2d(sp_emb, sp_shape, grid)
+    feats = nm.act(feats + nm.param(sp_emb))                # :514
+
+    feats = stacked_transformer(feats, patches_paddings,
+                                params["spatial_encoder"]["transformers_stack"], nm,
+                                cfg["num_spatial_layers"], heads, cap)
+    feats = layer_norm(feats, params["spatial_ln"]["scale"], params["spatial_ln"]["bias"], nm)
+    spatial_features = feats
+    n = feats.shape[1]
+    feats = feats.reshape(b, t, n, D).transpose(0, 2, 1, 3).reshape(b * n, t, D)  # :535
+    temporal_paddings = None
+    if patches_paddings is not None:
+        temporal_paddings = patches_paddings.reshape(b, t, n).transpose(0, 2, 1).reshape(b * n, t)
+
+    t_len = cfg["pos_emb_shape"][0]
+    t_emb = np.asarray(params["temporal_pos_emb"]["emb_var"], dtype=np.float64)[:t_len][None]
+    if t_len != t:
+        t_emb = interpolate_emb_1d(t_emb, t)                # :551-552
+    feats = nm.act(feats + nm.param(t_emb))
+
+    feats = stacked_transformer(feats, temporal_paddings,
+                                params["temporal_encoder"]["transformers_stack"], nm,
+                                cfg["num_temporal_layers"], heads, cap)
+    feats = layer_norm(feats, params["temporal_ln"]["scale"], params["temporal_ln"]["bias"], nm)
+    feats = feats.reshape(b, n, t, D).transpose(0, 2, 1, 3).reshape(b, t * n, D)  # :570
+
+    outputs = {}
+    if _contains(return_intermediate, "spatial_features"):
+        outputs["spatial_features"] = spatial_features.reshape(b, t * n, D)     # :575-578
+    return feats, outputs
+
+
+# --------------------------------------------------------------------------- #
+# op-level restatements used by the kernel unit tests
+# --------------------------------------------------------------------------- #
+def capped_softmax_attention(q, k, v, cap: float, key_mask=None):
+    """Per-problem attention used to check the HIP attention kernels.
+
+    q,k,v: [P, S, dh] with q already scaled (layers.py:569-584).  Returns [P, S, dh].
+    key_mask: optional [P, S] (1 = padded key).  Follows layers.py:586-661.
+    """
+    logits = np.matmul(q, np.swapaxes(k, -1, -2))
+    if cap > 0:
+        logits = cap * np.tanh(logits / cap)
+    if key_mask is not None:
+        logits = apply_mask_to_logits(logits, padding_mask(key_mask)[:, 0])
+    return np.matmul(softmax(logits), v)

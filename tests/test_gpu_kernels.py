@@ -1,0 +1,240 @@
+"""Op-level parity of the HIP kernels (through the C-ABI op entry points) against
+plain PyTorch fp32/fp64 references and the NumPy oracle.
+
+Tolerances:
+  * bf16 GEMM: operands are exactly representable bf16, accumulation fp32 -> fp32 outputs
+    agree with an fp64 matmul of the same operands to ~1e-6 relative (1e-4 abs at O(1)
+    scale); bf16 outputs additionally carry one bf16 rounding (rtol 2^-8).
+  * fp32 GEMM (v_mfma_f32_16x16x4_f32): 2e-5 abs at O(1) scale for K <= 3072.
+  * bf16 attention: P is rounded to bf16 before P.V (as the reference's bf16 mode rounds
+    probs, layers.py:654): 1e-2 abs on O(1) values.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from videoprism import _native as nat
+from oracle import videoprism_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 768), (1024, 2304, 768), (256, 768, 3072), (512, 1024, 1024)])
+def test_gemm_bf16_store(cuda, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda) * 0.1
+    ab, wb = _bf(a), _bf(w)
+    ref = ab.double() @ wb.double().T + b.double()
+    out = nat.op_gemm(ab, wb, b, nat.EPI_STORE)
+    torch.cuda.synchronize()
+    assert out.dtype == torch.bfloat16
+    err = (out.double() - ref).abs()
+    assert torch.all(err <= 2 ** -8 * ref.abs() + 1e-3), float(err.max())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 3072, 768), (256, 256, 128)])
+def test_gemm_bf16_gelu_rowpad(cuda, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(7)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.25).float().to(cuda)
+    out = nat.op_gemm(a, w, b, nat.EPI_GELU, rowpad=pad)
+    torch.cuda.synchronize()
+    y = a.double() @ w.double().T + b.double()
+    ref = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) * (1 - pad.double())[:, None]
+    err = (out.double() - ref).abs()
+    assert torch.all(err <= 2 ** -8 * ref.abs() + 1e-3), float(err.max())
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (256, 768, 3072)])
+def test_gemm_bf16_resid_inplace(cuda, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(11)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    x = torch.randn(M, N, generator=g).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.25).float().to(cuda)
+    ref = x.double() + (a.double() @ w.double().T + b.double()) * (1 - pad.double())[:, None]
+    nat.op_gemm(a, w, b, nat.EPI_RESID, out=x, resid=x, rowpad=pad)
+    torch.cuda.synchronize()
+    assert float((x.double() - ref).abs().max()) < 1e-4
+
+
+def test_gemm_bf16_pos(cuda):
+    M, N, K = 1024, 768, 1024
+    g = torch.Generator(device="cpu").manual_seed(5)
+    a = _bf(torch.rand(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pos = torch.randn(256, N, generator=g).to(cuda)
+    out = nat.op_gemm(a, w, b, nat.EPI_POS, pos=pos)
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().T + b.double() + pos.double().repeat(M // 256, 1)
+    assert float((out.double() - ref).abs().max()) < 1e-4
+
+
+def test_gemm_bf16_asymmetric_identity(cuda):
+    """A = I with an asymmetric W catches a transposed C write (guide §3)."""
+    M = N = K = 256
+    a = _bf(torch.eye(M)).to(cuda)
+    w = _bf(torch.arange(N * K, dtype=torch.float32).reshape(N, K) % 97 - 48).to(cuda)
+    b = torch.zeros(N, device=cuda)
+    out = nat.op_gemm(a, w, b, nat.EPI_RESID, out=torch.zeros(M, N, device=cuda),
+                      resid=torch.zeros(M, N, device=cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(out, w.float().T.contiguous())
+
+
+@pytest.mark.parametrize("epi", [nat.EPI_STORE, nat.EPI_GELU, nat.EPI_RESID, nat.EPI_POS])
+def test_gemm_f32(cuda, epi):
+    M, N, K = 512, 768, 3072 if epi == nat.EPI_RESID else 768
+    g = torch.Generator(device="cpu").manual_seed(epi)
+    a = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.25).float().to(cuda)
+    x = torch.randn(M, N, generator=g).to(cuda)
+    pos = torch.randn(256, N, generator=g).to(cuda)
+    y = a.double() @ w.double().T + b.double()
+    if epi == nat.EPI_STORE:
+        out, ref = nat.op_gemm(a, w, b, epi), y
+    elif epi == nat.EPI_GELU:
+        out = nat.op_gemm(a, w, b, epi, rowpad=pad)
+        ref = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) * (1 - pad.double())[:, None]
+    elif epi == nat.EPI_RESID:
+        ref = x.double() + y * (1 - pad.double())[:, None]
+        out = nat.op_gemm(a, w, b, epi, out=x, resid=x, rowpad=pad)
+    else:
+        out = nat.op_gemm(a, w, b, epi, pos=pos)
+        ref = y + pos.double().repeat(M // 256, 1)
+    torch.cuda.synchronize()
+    assert float((out.double() - ref).abs().max()) < 2e-5
+
+
+def _qkv(num_seq, S, heads, seed, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    D = heads * 64
+    q = torch.randn(num_seq * S, D, generator=g) * scale * 0.125 * 8
+    k = torch.randn(num_seq * S, D, generator=g) * scale
+    v = torch.randn(num_seq * S, D, generator=g)
+    return torch.cat([q, k, v], dim=1)
+
+
+def _oracle_attention(qkv, num_seq, S, heads, cap, key_pad=None):
+    D = heads * 64
+    x = qkv.double().cpu().numpy().reshape(num_seq, S, 3, heads, 64)
+    q = x[:, :, 0].transpose(0, 2, 1, 3).reshape(num_seq * heads, S, 64)
+    k = x[:, :, 1].transpose(0, 2, 1, 3).reshape(num_seq * heads, S, 64)
+    v = x[:, :, 2].transpose(0, 2, 1, 3).reshape(num_seq * heads, S, 64)
+    kp = None
+    if key_pad is not None:
+        kp = np.repeat(key_pad.cpu().numpy().reshape(num_seq, 1, S), heads, axis=1).reshape(-1, S)
+    o = orc.capped_softmax_attention(q, k, v, cap, kp)
+    return o.reshape(num_seq, heads, S, 64).transpose(0, 2, 1, 3).reshape(num_seq * S, D)
+
+
+@pytest.mark.parametrize("S,num_seq,heads,scale", [(256, 3, 12, 1.0), (256, 2, 16, 4.0),
+                                                   (16, 40, 12, 1.0), (8, 9, 12, 3.0), (5, 7, 16, 1.0)])
+def test_attention_bf16(cuda, S, num_seq, heads, scale):
+    qkv = _bf(_qkv(num_seq, S, heads, S + num_seq, scale)).to(cuda)
+    out = nat.op_attention(qkv, num_seq, S, heads, 50.0)
+    torch.cuda.synchronize()
+    ref = _oracle_attention(qkv, num_seq, S, heads, 50.0)
+    err = np.abs(out.double().cpu().numpy() - ref)
+    # bound: bf16 rounding of the output (2^-9 |o|) + of each numerator before P.V
+    # (2^-9 * max|v|), doubled for accumulation slack
+    vmax = float(qkv[:, 2 * heads * 64:].float().abs().max())
+    assert np.all(err <= 2 ** -8 * (np.abs(ref) + vmax)), err.max()
+    assert err.mean() < 2e-3, err.mean()
+
+
+@pytest.mark.parametrize("S,num_seq", [(256, 3), (16, 10), (8, 6)])
+def test_attention_bf16_key_padding(cuda, S, num_seq):
+    heads = 12
+    qkv = _bf(_qkv(num_seq, S, heads, 3)).to(cuda)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    if S == 256:  # spatial stage: a padded frame pads all of its keys
+        kp = torch.zeros(num_seq, S)
+        kp[1] = 1.0
+    else:
+        kp = (torch.rand(num_seq, S, generator=g) < 0.4).float()
+        kp[0] = 1.0  # fully padded sequence -> uniform attention
+    kp = kp.reshape(-1).to(cuda)
+    out = nat.op_attention(qkv, num_seq, S, heads, 50.0, key_pad=kp)
+    torch.cuda.synchronize()
+    ref = _oracle_attention(qkv, num_seq, S, heads, 50.0, kp.reshape(num_seq, S))
+    err = np.abs(out.double().cpu().numpy() - ref)
+    vmax = float(qkv[:, 2 * heads * 64:].float().abs().max())
+    assert np.all(err <= 2 ** -8 * (np.abs(ref) + vmax)), err.max()
+
+
+@pytest.mark.parametrize("S,num_seq,heads", [(256, 2, 12), (16, 20, 12), (4, 3, 16)])
+def test_attention_f32(cuda, S, num_seq, heads):
+    qkv = _qkv(num_seq, S, heads, 17, 2.0).to(cuda)
+    kp = torch.zeros(num_seq, S)
+    kp[-1, : S // 2] = 1.0
+    out = nat.op_attention(qkv, num_seq, S, heads, 50.0, key_pad=kp.reshape(-1).to(cuda))
+    torch.cuda.synchronize()
+    ref = _oracle_attention(qkv, num_seq, S, heads, 50.0, kp)
+    # logits here reach |q.k| ~ 100 (scale 2): fp32 ulp there is ~8e-6, so the probabilities
+    # carry ~1e-5 relative error by construction; bound 3e-5 on O(1) outputs.
+    assert np.abs(out.double().cpu().numpy() - ref).max() < 3e-5
+
+
+@pytest.mark.parametrize("D,perm", [(768, nat.PERM_NONE), (768, nat.PERM_BTN_TO_BNT),
+                                    (1024, nat.PERM_BNT_TO_BTN)])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_layernorm(cuda, D, perm, out_bf16):
+    B, T, N = 2, 4, 256
+    g = torch.Generator(device="cpu").manual_seed(D + perm)
+    x = (torch.randn(B * T * N, D, generator=g) * 3 + 1).to(cuda)
+    scale = torch.randn(D, generator=g) * 0.1
+    bias = torch.randn(D, generator=g) * 0.1
+    add = torch.randn(T, D, generator=g).to(cuda) if perm == nat.PERM_BTN_TO_BNT else None
+    out = nat.op_layernorm(x, (1 + scale).to(cuda), bias.to(cuda),
+                           torch.bfloat16 if out_bf16 else torch.float32, perm, T, N, add)
+    torch.cuda.synchronize()
+    xd = x.double().cpu().numpy()
+    ref = orc.layer_norm(xd, scale.double().numpy(), bias.double().numpy(), orc.Numerics("f64"))
+    if perm == nat.PERM_BTN_TO_BNT:
+        ref = ref.reshape(B, T, N, D).transpose(0, 2, 1, 3) + add.double().cpu().numpy()[None, None]
+        ref = ref.reshape(-1, D)
+    elif perm == nat.PERM_BNT_TO_BTN:
+        ref = ref.reshape(B, N, T, D).transpose(0, 2, 1, 3).reshape(-1, D)
+    err = np.abs(out.double().cpu().numpy() - ref)
+    tol = 2 ** -8 * np.abs(ref) + 1e-5 if out_bf16 else 2e-5
+    assert np.all(err <= tol), err.max()
+
+
+@pytest.mark.parametrize("in_bf16", [False, True])
+def test_patchify(cuda, in_bf16):
+    BT, H, P = 3, 288, 18
+    g = torch.Generator(device="cpu").manual_seed(1)
+    v = torch.rand(BT, H, H, 3, generator=g)
+    if in_bf16:
+        v = _bf(v)
+    vd = v.to(cuda)
+    out = nat.op_patchify(vd, P, 1024, torch.bfloat16)
+    torch.cuda.synchronize()
+    ref = orc.image_to_patch(v.float().numpy(), P).reshape(-1, P * P * 3)
+    got = out.float().cpu().numpy()
+    np.testing.assert_array_equal(got[:, P * P * 3:], 0)
+    np.testing.assert_array_equal(got[:, : P * P * 3], orc.round_bf16(ref))
+
+
+def test_pool_l2(cuda):
+    g = torch.Generator(device="cpu").manual_seed(2)
+    e = torch.randn(3, 4096, 768, generator=g).to(cuda)
+    out = nat.op_pool_l2(e)
+    torch.cuda.synchronize()
+    m = e.double().mean(1)
+    ref = m / torch.sqrt((m * m).sum(-1, keepdim=True) + 1e-12)
+    assert float((out.double() - ref).abs().max()) < 1e-6

@@ -1,0 +1,395 @@
+// Capped dot-product attention for the factorized encoder.
+//
+// Reference semantics (layers.py:601-661, _cap_logits :586-594, masks :51-89):
+//   logits = q.k (q pre-scaled by dh^-0.5, folded into the q projection weights)
+//   logits = cap * tanh(logits / cap); softmax in fp32; probs . v
+// Because |cap*tanh(.)| <= cap (= 50 on every VideoPrism config), exp(logit) lies in
+// [e^-50, e^50] and the softmax needs no running max: numerators are exp(x) directly and
+// the row sum is exact in fp32.  Padded keys (key_pad = 1) contribute 0; if every key of a
+// row is padded, the reference's where(mask, logits, -0.7*FLT_MAX) makes all logits equal
+// and softmax uniform -- reproduced by treating every key as weight 1.
+//
+// attention_spatial_bf16: S = 256 (one frame's patch grid), dh = 64.  One workgroup per
+//   (frame, head); K and V (32 KiB each) land in LDS by global_load_lds; 8 waves x 32
+//   queries.  S^T = K.Q^T on v_mfma_f32_32x32x16_bf16 puts one query per lane column; the
+//   bf16 numerators are fed straight back as the B operand of O^T = V^T.P^T (V read with
+//   ds_read_b64_tr_b16), so P never touches LDS and the row sum is lane-local.
+// attention_temporal_bf16: S = T <= 16 frames.  One wave per (sequence, head), 16x16x32 for
+//   Q.K^T and 16x16x16 for P.V; memory-bound on the qkv rows.
+// attention_f32: generic fp32 path (fprop_dtype=float32), online softmax, exact tanhf/expf.
+#include "vp_common.h"
+#include "vp_kernels.h"
+
+namespace vp {
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+// exp(cap * tanh(x / cap)) with tanh(y) = 1 - 2 / (exp(2y) + 1); saturates correctly.
+__device__ __forceinline__ float capped_exp(float x, float two_log2e_over_cap, float cap_log2e) {
+  const float t = __builtin_amdgcn_exp2f(x * two_log2e_over_cap);
+  const float r = __builtin_amdgcn_rcpf(t + 1.0f);
+  return __builtin_amdgcn_exp2f(cap_log2e - 2.0f * cap_log2e * r);
+}
+
+__device__ __forceinline__ int swzK(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int swzV(int row) { return ((row >> 1) & 1) << 2; }
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x4 tr_read(const char* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+  return bf16x4{v[0], v[1], v[2], v[3]};
+}
+
+// ------------------------------------------------------------------------------------
+// spatial: S = 256, dh = 64
+// ------------------------------------------------------------------------------------
+constexpr int kSpS = 256;
+constexpr int kSpThreads = 512;
+constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
+
+template <bool MASK>
+__global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
+    const float* __restrict__ key_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ks = smem;
+  char* Vs = smem + kSpS * 128;
+  float* kp = reinterpret_cast<float*>(smem + 2 * kSpS * 128);
+  int* allmask = reinterpret_cast<int*>(kp + kSpS);
+
+  const int D = heads * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const int seq = blockIdx.x / heads;
+  const int h = blockIdx.x % heads;
+  const int lane = threadIdx.x & 63;
+  const int w = wave_id();
+  const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * 64;
+
+  // ---- stage K (pieces 0..31) and V (32..63): 8 pieces of 8 rows x 128 B per wave ----
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = w * 8 + i;
+    const bool isV = piece >= 32;
+    const int row = (piece & 31) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
+    const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * D : D) + c * 8;
+    __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
+  }
+  // ---- this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j) ----
+  const int q0 = w * 32;
+  const int half = lane >> 5;
+  bf16x8 qf[4];
+  {
+    const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) qf[kd] = *reinterpret_cast<const bf16x8*>(qp + 16 * kd);
+  }
+  if constexpr (MASK) {
+    if (threadIdx.x < kSpS) kp[threadIdx.x] = key_pad[(int64_t)seq * kSpS + threadIdx.x];
+    if (threadIdx.x == 0) *allmask = 1;
+  }
+  wait_vmcnt0();
+  __syncthreads();
+  bool all_masked = false;
+  if constexpr (MASK) {
+    if (threadIdx.x < kSpS && kp[threadIdx.x] == 0.0f) *allmask = 0;
+    __syncthreads();
+    all_masked = *allmask != 0;
+  }
+
+  const float c1 = 2.0f * kLog2e / cap;
+  const float c2 = cap * kLog2e;
+  f32x16 y0 = {}, y1 = {};
+  float lsum = 0.0f;
+  const int krow_l = lane & 31;
+  const int g = lane >> 4;
+  const int li = lane & 15;
+  const int trq = li >> 2, trp = li & 3;
+
+#pragma unroll 2
+  for (int kt = 0; kt < kSpS / 32; ++kt) {
+    // S^T tile: X[key][q], keys kt*32 .. +31
+    f32x16 x = {};
+    const int krow = kt * 32 + krow_l;
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) {
+      const int c = 2 * kd + half;
+      const bf16x8 kf =
+          *reinterpret_cast<const bf16x8*>(Ks + krow * 128 + ((c ^ swzK(krow)) << 4));
+      x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kd], x, 0, 0, 0);
+    }
+    // numerators: register i <-> key kt*32 + (i&3) + 8(i>>2) + 4*half
+    float p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float e = capped_exp(x[i], c1, c2);
+      if constexpr (MASK) {
+        const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
+        e = all_masked ? 1.0f : (kp[key] != 0.0f ? 0.0f : e);
+      }
+      p[i] = e;
+      lsum += e;
+    }
+    bf16x8 pf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      uint32_t u[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) u[j] = pack_bf16x2(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
+      pf[s] = *reinterpret_cast<bf16x8*>(u);
+    }
+    // O^T += V^T . X  (A = V^T via transposed reads, B = P^T numerators)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int key = kt * 32 + 16 * s + 4 * half + trq;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
+        const int c = col >> 3;
+        const char* ad = Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2;
+        const bf16x4 lo = tr_read(ad);
+        const bf16x4 hi = tr_read(ad + 8 * 128);
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dh == 0)
+          y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y0, 0, 0, 0);
+        else
+          y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y1, 0, 0, 0);
+      }
+    }
+  }
+  lsum += __shfl_xor(lsum, 32);
+  const float inv = 1.0f / lsum;
+  // y_dh[i] = O^T[d = 32dh + (i&3) + 8(i>>2) + 4*half][q = q0 + (l&31)]
+  bf16_t* op = o + ((int64_t)seq * kSpS + q0 + (lane & 31)) * D + h * 64 + 4 * half;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    uint2 v0 = make_uint2(pack_bf16x2(y0[4 * g4] * inv, y0[4 * g4 + 1] * inv),
+                          pack_bf16x2(y0[4 * g4 + 2] * inv, y0[4 * g4 + 3] * inv));
+    uint2 v1 = make_uint2(pack_bf16x2(y1[4 * g4] * inv, y1[4 * g4 + 1] * inv),
+                          pack_bf16x2(y1[4 * g4 + 2] * inv, y1[4 * g4 + 3] * inv));
+    *reinterpret_cast<uint2*>(op + 8 * g4) = v0;
+    *reinterpret_cast<uint2*>(op + 32 + 8 * g4) = v1;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// temporal: S <= 16, dh = 64; one wave per (sequence, head)
+// ------------------------------------------------------------------------------------
+constexpr int kTpWaves = 4;
+
+template <bool MASK>
+__global__ __launch_bounds__(kTpWaves * 64) void attn_temporal_kernel(
+    const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int num_pairs, int S, int heads,
+    float cap, const float* __restrict__ key_pad) {
+  __shared__ __attribute__((aligned(16))) char vlds[kTpWaves * 16 * 128];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int pair = blockIdx.x * kTpWaves + w;
+  if (pair >= num_pairs) return;  // whole wave exits together
+  const int seq = pair / heads;
+  const int h = pair % heads;
+  const int D = heads * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const bf16_t* base = qkv + (int64_t)seq * S * ld + h * 64;
+  char* vs = vlds + w * 16 * 128;
+
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+  // Q/K fragments (16x16x32): lane row r16, d = 32ks + 8g + j
+  bf16x8 qf[2], kf[2];
+  const bool rv = r16 < S;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    if (rv) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(base + (int64_t)r16 * ld + 32 * ks + 8 * g);
+      kf[ks] = *reinterpret_cast<const bf16x8*>(base + (int64_t)r16 * ld + D + 32 * ks + 8 * g);
+    } else {
+      qf[ks] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      kf[ks] = qf[ks];
+    }
+  }
+  // V rows -> LDS [16][64] (row 128 B): lane covers row lane>>3 (+8), chunk lane&7
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = i * 8 + (lane >> 3);
+    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (row < S) v = *reinterpret_cast<const bf16x8*>(base + (int64_t)row * ld + 2 * D + (lane & 7) * 8);
+    *reinterpret_cast<bf16x8*>(vs + row * 128 + (lane & 7) * 16) = v;
+  }
+  f32x4 x = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) x = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[ks], qf[ks], x, 0, 0, 0);
+  // x[r] = S^T[key = 4g + r][q = r16]
+  bool all_masked = false;
+  float kpad[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MASK) {
+    // every lane evaluates the whole key set of its sequence (S <= 16 floats)
+    int nvalid = 0;
+    for (int k = 0; k < S; ++k) nvalid += key_pad[(int64_t)seq * S + k] == 0.0f;
+    all_masked = nvalid == 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 4 * g + r;
+      kpad[r] = key < S ? key_pad[(int64_t)seq * S + key] : 1.0f;
+    }
+  }
+  const float c1 = 2.0f * kLog2e / cap;
+  const float c2 = cap * kLog2e;
+  float p[4];
+  float lsum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int key = 4 * g + r;
+    float e = key < S ? capped_exp(x[r], c1, c2) : 0.0f;
+    if constexpr (MASK) e = key < S ? (all_masked ? 1.0f : (kpad[r] != 0.0f ? 0.0f : e)) : 0.0f;
+    p[r] = e;
+    lsum += e;
+  }
+  lsum += __shfl_xor(lsum, 16);
+  lsum += __shfl_xor(lsum, 32);
+  const float inv = 1.0f / lsum;
+  uint32_t pu[2] = {pack_bf16x2(p[0], p[1]), pack_bf16x2(p[2], p[3])};
+  const bf16x4 pb = *reinterpret_cast<bf16x4*>(pu);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): V rows written by this wave
+  __builtin_amdgcn_wave_barrier();
+  const int trq = r16 >> 2, trp = r16 & 3;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    // A = V^T: lane (d = 16dt + r16) x keys 4g..4g+3 via transposed read
+    const bf16x4 vf = tr_read(vs + (4 * g + trq) * 128 + (16 * dt + 4 * trp) * 2);
+    f32x4 y = {0.f, 0.f, 0.f, 0.f};
+    y = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pb, y, 0, 0, 0);
+    // y[r] = O^T[d = 16dt + 4g + r][q = r16]
+    if (rv) {
+      uint2 st = make_uint2(pack_bf16x2(y[0] * inv, y[1] * inv), pack_bf16x2(y[2] * inv, y[3] * inv));
+      *reinterpret_cast<uint2*>(o + ((int64_t)seq * S + r16) * D + h * 64 + 16 * dt + 4 * g) = st;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// fp32 generic (fprop_dtype=float32): one workgroup per (sequence, head), one query per
+// thread, K/V of the sequence in LDS, online softmax with exact tanhf/expf.
+// ------------------------------------------------------------------------------------
+constexpr int kF32MaxS = 256;
+
+__global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__ qkv,
+                                                        float* __restrict__ o, int S, int heads,
+                                                        float cap,
+                                                        const float* __restrict__ key_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Ks = reinterpret_cast<float*>(smem);        // [S][64]
+  float* Vs = Ks + S * 64;                            // [S][64]
+  float* kp = Vs + S * 64;                            // [S]
+  int& nvalid = *reinterpret_cast<int*>(kp + S);
+  const int D = heads * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const int seq = blockIdx.x / heads;
+  const int h = blockIdx.x % heads;
+  const float* base = qkv + (int64_t)seq * S * ld + h * 64;
+  if (threadIdx.x == 0) nvalid = 0;
+  for (int i = threadIdx.x; i < S * 16; i += blockDim.x) {
+    const int row = i >> 4, c4 = (i & 15) * 4;
+    *reinterpret_cast<float4*>(Ks + row * 64 + c4) =
+        *reinterpret_cast<const float4*>(base + (int64_t)row * ld + D + c4);
+    *reinterpret_cast<float4*>(Vs + row * 64 + c4) =
+        *reinterpret_cast<const float4*>(base + (int64_t)row * ld + 2 * D + c4);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < S; i += blockDim.x) {
+    const float pv = key_pad ? key_pad[(int64_t)seq * S + i] : 0.0f;
+    kp[i] = pv;
+    if (pv == 0.0f) atomicAdd(&nvalid, 1);
+  }
+  __syncthreads();
+  const bool all_masked = nvalid == 0;
+  const int qi = threadIdx.x;
+  if (qi >= S) return;
+  float q[64];
+#pragma unroll
+  for (int d = 0; d < 64; d += 4) {
+    const float4 t = *reinterpret_cast<const float4*>(base + (int64_t)qi * ld + d);
+    q[d] = t.x; q[d + 1] = t.y; q[d + 2] = t.z; q[d + 3] = t.w;
+  }
+  float acc[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) acc[d] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < S; ++j) {
+    if (!all_masked && kp[j] != 0.0f) continue;
+    float s = 0.f;
+    if (!all_masked) {
+#pragma unroll
+      for (int d = 0; d < 64; ++d) s = fmaf(q[d], Ks[j * 64 + d], s);
+      if (cap > 0.f) s = cap * tanhf(s / cap);
+    }
+    const float mn = fmaxf(m, s);
+    const float sc = expf(m - mn);
+    const float e = expf(s - mn);
+    l = l * sc + e;
+#pragma unroll
+    for (int d = 0; d < 64; ++d) acc[d] = fmaf(acc[d], sc, e * Vs[j * 64 + d]);
+    m = mn;
+  }
+  const float inv = 1.0f / l;
+  float* op = o + ((int64_t)seq * S + qi) * D + h * 64;
+#pragma unroll
+  for (int d = 0; d < 64; d += 4)
+    *reinterpret_cast<float4*>(op + d) =
+        make_float4(acc[d] * inv, acc[d + 1] * inv, acc[d + 2] * inv, acc[d + 3] * inv);
+}
+
+}  // namespace
+
+hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads, float cap,
+                                  const float* key_pad, hipStream_t s) {
+  if (!(cap > 0.0f)) return hipErrorInvalidValue;
+  static bool attr[2] = {false, false};
+  const int mi = key_pad ? 1 : 0;
+  const void* fn = key_pad ? (const void*)attn_spatial_kernel<true> : (const void*)attn_spatial_kernel<false>;
+  if (!attr[mi]) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
+    if (e != hipSuccess) return e;
+    attr[mi] = true;
+  }
+  const dim3 grid(num_seq * heads);
+  if (key_pad)
+    hipLaunchKernelGGL(attn_spatial_kernel<true>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad);
+  else
+    hipLaunchKernelGGL(attn_spatial_kernel<false>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad);
+  return hipGetLastError();
+}
+
+hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
+                                   float cap, const float* key_pad, hipStream_t s) {
+  if (!(cap > 0.0f) || S < 1 || S > 16) return hipErrorInvalidValue;
+  const int pairs = num_seq * heads;
+  const dim3 grid((pairs + kTpWaves - 1) / kTpWaves);
+  if (key_pad)
+    hipLaunchKernelGGL(attn_temporal_kernel<true>, grid, dim3(kTpWaves * 64), 0, s, qkv, o, pairs, S, heads, cap, key_pad);
+  else
+    hipLaunchKernelGGL(attn_temporal_kernel<false>, grid, dim3(kTpWaves * 64), 0, s, qkv, o, pairs, S, heads, cap, key_pad);
+  return hipGetLastError();
+}
+
+hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
+                         const float* key_pad, hipStream_t s) {
+  if (S < 1 || S > kF32MaxS) return hipErrorInvalidValue;
+  static bool attr = false;
+  const int lds = (2 * S * 64 + S) * 4 + 16;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)attn_f32_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (2 * kF32MaxS * 64 + kF32MaxS) * 4 + 16);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(attn_f32_kernel, dim3(num_seq * heads), dim3(256), lds, s, qkv, o, S, heads, cap, key_pad);
+  return hipGetLastError();
+}
+
+}  // namespace vp

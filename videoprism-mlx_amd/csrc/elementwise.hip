@@ -1,0 +1,255 @@
+// HBM-bound kernels of the encoder path: patchify, LayerNorm (+row permutation and
+// positional add), casts and padding expansion.
+#include "vp_common.h"
+#include "vp_kernels.h"
+
+namespace vp {
+
+namespace {
+
+// ---- patchify (encoders.py:70-104): '(m p)(n q) c -> (m n)(p q c)', K zero-padded ----
+// One thread produces 8 consecutive K elements of one patch row (a 16-byte store); the
+// 8 source elements are read from the NHWC frame (a run of P*C contiguous values per p).
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void patchify_kernel(const TI* __restrict__ video,
+                                                       TO* __restrict__ out, int BT, int H, int W,
+                                                       int C, int P, int kpad) {
+  const int gm = H / P, gn = W / P, np_ = gm * gn;
+  const int kreal = P * P * C;
+  const int64_t groups_per_row = kpad / 8;
+  const int64_t total = (int64_t)BT * np_ * groups_per_row;
+  for (int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gid < total;
+       gid += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = gid / groups_per_row;
+    const int k0 = (int)(gid % groups_per_row) * 8;
+    const int bt = (int)(row / np_);
+    const int pidx = (int)(row % np_);
+    const int mi = pidx / gn, ni = pidx % gn;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      float x = 0.0f;
+      if (k < kreal) {
+        const int p = k / (P * C);
+        const int rem = k - p * P * C;  // = q*C + c, contiguous in the source row
+        const int64_t off = (((int64_t)bt * H + mi * P + p) * W + ni * P) * C + rem;
+        if constexpr (sizeof(TI) == 2) x = bf2f(video[off]); else x = video[off];
+      }
+      v[j] = x;
+    }
+    if constexpr (sizeof(TO) == 2) {
+      uint4 o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                           pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      *reinterpret_cast<uint4*>(out + row * kpad + k0) = o;
+    } else {
+      float4* op = reinterpret_cast<float4*>(out + row * kpad + k0);
+      op[0] = make_float4(v[0], v[1], v[2], v[3]);
+      op[1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+}
+
+// ---- LayerNorm (layers.py:208-270) over fp32 rows, one wave per row ----
+// NCH = D / 256 float4 chunks per lane.  gamma = 1 + scale (folded on the host).
+template <int NCH, bool OUT_BF16>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int rows,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta,
+                                                        void* __restrict__ out, int perm, int T,
+                                                        int Nsp, const float* __restrict__ add) {
+  constexpr int D = NCH * 256;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * D;
+  float4 v[NCH];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    v[c] = *reinterpret_cast<const float4*>(xr + c * 256 + lane * 4);
+    s += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+  const float mean = s * (1.0f / D);
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    v[c].x -= mean; v[c].y -= mean; v[c].z -= mean; v[c].w -= mean;
+    ss += (v[c].x * v[c].x + v[c].y * v[c].y) + (v[c].z * v[c].z + v[c].w * v[c].w);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off);
+  const float rstd = 1.0f / sqrtf(ss * (1.0f / D) + 1e-6f);
+
+  int64_t orow = row;
+  int t_of_out = 0;
+  if (perm == PERM_BTN_TO_BNT) {  // r = (b*T + t)*Nsp + n  ->  (b*Nsp + n)*T + t
+    const int n = row % Nsp;
+    const int bt = row / Nsp;
+    const int t = bt % T, b = bt / T;
+    orow = ((int64_t)b * Nsp + n) * T + t;
+    t_of_out = t;
+  } else if (perm == PERM_BNT_TO_BTN) {  // r = (b*Nsp + n)*T + t  ->  (b*T + t)*Nsp + n
+    const int t = row % T;
+    const int bn = row / T;
+    const int n = bn % Nsp, b = bn / Nsp;
+    orow = ((int64_t)b * T + t) * Nsp + n;
+    t_of_out = t;
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    const float4 gm = *reinterpret_cast<const float4*>(gamma + col);
+    const float4 bt = *reinterpret_cast<const float4*>(beta + col);
+    float4 y = make_float4(v[c].x * rstd * gm.x + bt.x, v[c].y * rstd * gm.y + bt.y,
+                           v[c].z * rstd * gm.z + bt.z, v[c].w * rstd * gm.w + bt.w);
+    if (add) {
+      const float4 a = *reinterpret_cast<const float4*>(add + (int64_t)t_of_out * D + col);
+      y.x += a.x; y.y += a.y; y.z += a.z; y.w += a.w;
+    }
+    if constexpr (OUT_BF16) {
+      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + orow * D + col) =
+          make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+    } else {
+      *reinterpret_cast<float4*>(static_cast<float*>(out) + orow * D + col) = y;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x,
+                                                            bf16_t* __restrict__ y, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<uint2*>(y)[i] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  }
+}
+
+__global__ __launch_bounds__(256) void expand_paddings_kernel(const float* __restrict__ fp, int B,
+                                                              int T, int Nsp,
+                                                              float* __restrict__ pad_btn,
+                                                              float* __restrict__ pad_bnt) {
+  const int64_t total = (int64_t)B * T * Nsp;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    // i in (b, t, n) order
+    const int n = (int)(i % Nsp);
+    const int64_t bt = i / Nsp;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    const float v = fp[bt];
+    pad_btn[i] = v;
+    pad_bnt[((int64_t)b * Nsp + n) * T + t] = v;
+  }
+}
+
+
+// ---- pooled clip embedding: out[b] = l2norm(mean_l emb[b, l, :]) (encoders.py:50-67) ----
+template <typename T>
+__global__ __launch_bounds__(256) void pool_l2_kernel(const T* __restrict__ emb, int L, int D,
+                                                      float* __restrict__ out) {
+  __shared__ float red[256 / 64];
+  const int b = blockIdx.x;
+  const T* e = emb + (int64_t)b * L * D;
+  float sq = 0.f;
+  for (int col = threadIdx.x; col < D; col += blockDim.x) {
+    float s = 0.f;
+    for (int l = 0; l < L; ++l) {
+      if constexpr (sizeof(T) == 2) s += bf2f(e[(int64_t)l * D + col]); else s += e[(int64_t)l * D + col];
+    }
+    s *= 1.0f / L;
+    out[(int64_t)b * D + col] = s;
+    sq += s * s;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float inv = 1.0f / sqrtf(tot + 1e-12f);
+  for (int col = threadIdx.x; col < D; col += blockDim.x) out[(int64_t)b * D + col] *= inv;
+}
+
+int grid_for(int64_t work, int block) {
+  int64_t g = (work + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+template <int NCH>
+hipError_t ln_launch(const float* x, int rows, const float* gamma, const float* beta, void* out,
+                     int out_is_bf16, int perm, int T, int Nsp, const float* add, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  if (out_is_bf16)
+    hipLaunchKernelGGL((layernorm_kernel<NCH, true>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+                       out, perm, T, Nsp, add);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<NCH, false>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+                       out, perm, T, Nsp, add);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is_bf16, int BT, int H,
+                    int W, int C, int P, int kpad, hipStream_t s) {
+  if (kpad % 8 || kpad < P * P * C || H % P || W % P) return hipErrorInvalidValue;
+  const int64_t work = (int64_t)BT * (H / P) * (W / P) * (kpad / 8);
+  const int grid = grid_for(work, 256);
+  if (in_is_bf16) {
+    if (out_is_bf16)
+      hipLaunchKernelGGL((patchify_kernel<bf16_t, bf16_t>), dim3(grid), dim3(256), 0, s,
+                         (const bf16_t*)video, (bf16_t*)patches, BT, H, W, C, P, kpad);
+    else
+      hipLaunchKernelGGL((patchify_kernel<bf16_t, float>), dim3(grid), dim3(256), 0, s,
+                         (const bf16_t*)video, (float*)patches, BT, H, W, C, P, kpad);
+  } else {
+    if (out_is_bf16)
+      hipLaunchKernelGGL((patchify_kernel<float, bf16_t>), dim3(grid), dim3(256), 0, s,
+                         (const float*)video, (bf16_t*)patches, BT, H, W, C, P, kpad);
+    else
+      hipLaunchKernelGGL((patchify_kernel<float, float>), dim3(grid), dim3(256), 0, s,
+                         (const float*)video, (float*)patches, BT, H, W, C, P, kpad);
+  }
+  return hipGetLastError();
+}
+
+hipError_t layernorm(const float* x, int rows, int D, const float* gamma, const float* beta,
+                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add,
+                     hipStream_t s) {
+  switch (D) {
+    case 256: return ln_launch<1>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 512: return ln_launch<2>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 768: return ln_launch<3>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 1024: return ln_launch<4>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 1280: return ln_launch<5>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 1536: return ln_launch<6>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 2048: return ln_launch<8>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s) {
+  if (n % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, s, x, y, n / 4);
+  return hipGetLastError();
+}
+
+hipError_t expand_paddings(const float* frame_pad, int B, int T, int Nsp, float* pad_btn,
+                           float* pad_bnt, hipStream_t s) {
+  hipLaunchKernelGGL(expand_paddings_kernel, dim3(grid_for((int64_t)B * T * Nsp, 256)), dim3(256),
+                     0, s, frame_pad, B, T, Nsp, pad_btn, pad_bnt);
+  return hipGetLastError();
+}
+
+hipError_t pool_l2(const void* emb, int is_bf16, int B, int L, int D, float* out, hipStream_t s) {
+  if (is_bf16)
+    hipLaunchKernelGGL(pool_l2_kernel<bf16_t>, dim3(B), dim3(256), 0, s, (const bf16_t*)emb, L, D, out);
+  else
+    hipLaunchKernelGGL(pool_l2_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)emb, L, D, out);
+  return hipGetLastError();
+}
+
+}  // namespace vp

@@ -1,0 +1,67 @@
+// Internal (C++) launch interface of the HIP kernels.  The public C-ABI lives in
+// include/videoprism_hip.h and is implemented in vp_abi.cpp on top of these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vp {
+
+typedef uint16_t bf16_t;
+
+enum Epilogue {
+  EPI_BF16 = 0,       // out_bf16 = acc + bias                       (fused q|k|v projection)
+  EPI_GELU_BF16 = 1,  // out_bf16 = gelu(acc + bias) * (1 - rowpad)  (ffn_layer1)
+  EPI_RESID_F32 = 2,  // out_f32  = resid + (acc + bias) * (1 - rowpad)   (post, ffn_layer2)
+  EPI_POS_F32 = 3,    // out_f32  = acc + bias + pos[m % pos_rows]   (patch_projection + pos emb)
+};
+
+struct EpiArgs {
+  void* out = nullptr;
+  int64_t ldo = 0;
+  const float* bias = nullptr;    // [N]
+  const float* resid = nullptr;   // EPI_RESID_F32 (may alias out)
+  int64_t ldr = 0;
+  const float* pos = nullptr;     // EPI_POS_F32: [pos_rows][N]
+  int pos_rows = 1;
+  const float* rowpad = nullptr;  // optional [M], 1 = padded token
+};
+
+// ---- bf16 MFMA GEMM (gemm_bf16.hip) ----
+const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw);
+hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                     int N, int K, const EpiArgs& ep, hipStream_t s);
+
+// ---- fp32 GEMM for fprop_dtype=float32 (gemm_f32.hip) ----
+const char* gemm_f32_check(int M, int N, int K);
+hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_t ldw, int M,
+                    int N, int K, const EpiArgs& ep, hipStream_t s);
+
+// ---- attention (attention.hip) ----
+// qkv: rows of [q(D) | k(D) | v(D)], row r = seq * S + s; q pre-scaled by dh^-0.5.
+// o: rows of D = heads*64.  key_pad: optional [num_seq * S] (1 = padded key).
+hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
+                                  float cap, const float* key_pad, hipStream_t s);
+hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
+                                   float cap, const float* key_pad, hipStream_t s);
+hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
+                         const float* key_pad, hipStream_t s);
+
+// ---- elementwise / normalisation (elementwise.hip) ----
+enum RowPerm { PERM_NONE = 0, PERM_BTN_TO_BNT = 1, PERM_BNT_TO_BTN = 2 };
+// video [BT, H, W, C] (f32 or bf16) -> patches [BT*np, kpad] (bf16 or f32), zero-padded K.
+hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is_bf16, int BT,
+                    int H, int W, int C, int P, int kpad, hipStream_t s);
+// LayerNorm over D of fp32 rows; gamma already holds (1 + scale).  Output row r goes to
+// row perm(r); `add` (optional, fp32 [add_rows][D]) is added by the *output* row's t index.
+hipError_t layernorm(const float* x, int rows, int D, const float* gamma, const float* beta,
+                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add,
+                     hipStream_t s);
+// fp32 -> bf16 cast (weights are pre-packed on the host; this is for activations)
+hipError_t cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s);
+// per-token padding vector expansion: frame_pad [B*T] -> token pads in both orders
+hipError_t expand_paddings(const float* frame_pad, int B, int T, int Nsp, float* pad_btn,
+                           float* pad_bnt, hipStream_t s);
+
+hipError_t pool_l2(const void* emb, int is_bf16, int B, int L, int D, float* out, hipStream_t s);
+
+}  // namespace vp

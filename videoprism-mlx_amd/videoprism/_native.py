@@ -1,0 +1,196 @@
+"""ctypes binding of libvideoprism_hip.so (C-ABI declared in include/videoprism_hip.h).
+
+There is no fallback: if the library is missing or cannot be loaded, every entry point
+raises NativeLibraryError.  Device memory is passed as raw pointers of PyTorch-ROCm
+tensors; streams as hipStream_t handles of torch streams.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p
+
+_LIB_NAME = "libvideoprism_hip.so"
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
+
+VP_OK, VP_EINVAL, VP_ENOMEM, VP_EHIP, VP_ESTATE, VP_ENOTSUP = range(6)
+VP_F32, VP_BF16 = 0, 1
+
+EPI_STORE, EPI_GELU, EPI_RESID, EPI_POS = 0, 1, 2, 3
+PERM_NONE, PERM_BTN_TO_BNT, PERM_BNT_TO_BTN = 0, 1, 2
+
+
+class NativeLibraryError(RuntimeError):
+    """libvideoprism_hip.so is missing or failed to load (no CPU fallback exists)."""
+
+
+class VPError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[vp status {code}] {msg}")
+        self.code = code
+
+
+class vp_config(ctypes.Structure):
+    _fields_ = [
+        ("patch_size", c_int32),
+        ("pos_emb_t", c_int32),
+        ("pos_emb_h", c_int32),
+        ("pos_emb_w", c_int32),
+        ("model_dim", c_int32),
+        ("num_spatial_layers", c_int32),
+        ("num_temporal_layers", c_int32),
+        ("num_heads", c_int32),
+        ("mlp_dim", c_int32),
+        ("atten_logit_cap", c_float),
+        ("fprop_dtype", c_int32),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "vp_last_error": (c_char_p, []),
+    "vp_abi_version": (c_int, []),
+    "vp_create": (c_int, [POINTER(vp_config), c_int, POINTER(c_void_p)]),
+    "vp_destroy": (c_int, [c_void_p]),
+    "vp_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "vp_param_count": (c_int, [c_void_p, POINTER(c_int)]),
+    "vp_param_name": (c_int, [c_void_p, c_int, POINTER(c_char_p)]),
+    "vp_finalize": (c_int, [c_void_p]),
+    "vp_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "vp_forward": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p,
+                           c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "vp_op_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64,
+                           c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                           c_int64, c_void_p, c_void_p]),
+    "vp_op_attention": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
+                                c_void_p, c_void_p]),
+    "vp_op_layernorm": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int,
+                                c_int, c_int64, c_int64, c_void_p, c_void_p]),
+    "vp_op_patchify": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64,
+                               c_int64, c_int64, c_void_p]),
+    "vp_op_pool_l2": (c_int, [c_void_p, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Loads (once) and returns the library; raises NativeLibraryError if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise NativeLibraryError(
+            f"{_LIB_PATH} not found: build it with `make -C videoprism-mlx_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(_LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"failed to load {_LIB_PATH}: {e}") from e
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def check(rc: int) -> None:
+    if rc != VP_OK:
+        msg = load().vp_last_error().decode("utf-8", "replace")
+        if rc in (VP_EINVAL,):
+            raise ValueError(msg)
+        if rc == VP_ENOTSUP:
+            raise NotImplementedError(msg)
+        raise VPError(rc, msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args))
+
+
+# ---------------------------------------------------------------------------------------
+# torch-tensor helpers for the op-level entry points (used by kernel parity tests)
+# ---------------------------------------------------------------------------------------
+def _ptr(t):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def _stream(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return c_void_p(s.cuda_stream)
+
+
+def _prec(t):
+    import torch
+    if t.dtype == torch.bfloat16:
+        return VP_BF16
+    if t.dtype == torch.float32:
+        return VP_F32
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def op_gemm(a, w, bias, epilogue=EPI_STORE, out=None, resid=None, pos=None, rowpad=None,
+            stream=None):
+    """out = epilogue(a @ w.T + bias); a [M,K], w [N,K] (bf16 or fp32), bias fp32 [N]."""
+    import torch
+    M, K = a.shape
+    N = w.shape[0]
+    if out is None:
+        odt = a.dtype if epilogue in (EPI_STORE, EPI_GELU) else torch.float32
+        out = torch.empty((M, N), dtype=odt, device=a.device)
+    call("vp_op_gemm", _prec(a), epilogue, _ptr(a), a.stride(0), _ptr(w), w.stride(0), M, N, K,
+         _ptr(out), out.stride(0), _ptr(bias), _ptr(resid),
+         resid.stride(0) if resid is not None else 0, _ptr(pos),
+         pos.shape[0] if pos is not None else 0, _ptr(rowpad), _stream(stream))
+    return out
+
+
+def op_attention(qkv, num_seq, S, heads, cap, key_pad=None, out=None, stream=None):
+    import torch
+    D = heads * 64
+    if out is None:
+        out = torch.empty((num_seq * S, D), dtype=qkv.dtype, device=qkv.device)
+    call("vp_op_attention", _prec(qkv), _ptr(qkv), _ptr(out), num_seq, S, heads, float(cap),
+         _ptr(key_pad), _stream(stream))
+    return out
+
+
+def op_layernorm(x, gamma1p, beta, out_dtype=None, perm=PERM_NONE, T=1, Nsp=1, add=None,
+                 stream=None):
+    import torch
+    rows, D = x.shape
+    out_dtype = out_dtype or torch.float32
+    out = torch.empty((rows, D), dtype=out_dtype, device=x.device)
+    call("vp_op_layernorm", _ptr(x), rows, D, _ptr(gamma1p), _ptr(beta), _ptr(out),
+         VP_BF16 if out_dtype == torch.bfloat16 else VP_F32, perm, T, Nsp, _ptr(add),
+         _stream(stream))
+    return out
+
+
+def op_patchify(video, P, kpad, out_dtype=None, stream=None):
+    import torch
+    BT, H, W, C = video.shape
+    out_dtype = out_dtype or video.dtype
+    out = torch.empty((BT * (H // P) * (W // P), kpad), dtype=out_dtype, device=video.device)
+    call("vp_op_patchify", _ptr(video), _prec(video), _ptr(out),
+         VP_BF16 if out_dtype == torch.bfloat16 else VP_F32, BT, H, W, C, P, kpad, _stream(stream))
+    return out
+
+
+def op_pool_l2(emb, stream=None):
+    import torch
+    B, L, D = emb.shape
+    out = torch.empty((B, D), dtype=torch.float32, device=emb.device)
+    call("vp_op_pool_l2", _ptr(emb), _prec(emb), B, L, D, _ptr(out), _stream(stream))
+    return out

@@ -1,0 +1,118 @@
+"""Drop-in for videoprism/models_mlx.py (models_mlx.py:14-316) on MI355X.
+
+`load_video_encoder(name, weights_path)` returns a callable encoder:
+`model(video, return_intermediate=False, frame_paddings=None) -> (emb, outputs)`
+(encoders_mlx.py:502-543).  Weights: the files the reference's convert_weights.py
+writes (`weights/{name}_mlx.safetensors` or `.npz`, unstacked `layers/{i}` keys) or
+a Flax "repeated" npz; both are converted to the canonical scanned layout.
+"""
+
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+
+from . import encoders
+from . import params as params_lib
+from . import utils
+
+MODEL_CONFIGS = {
+    "videoprism_public_v1_base": {
+        "patch_size": 18, "pos_emb_shape": (16, 16, 16), "model_dim": 768,
+        "num_spatial_layers": 12, "num_temporal_layers": 4, "num_heads": 12, "mlp_dim": 3072,
+        "atten_logit_cap": 50.0, "norm_policy": "pre"},
+    "videoprism_public_v1_large": {
+        "patch_size": 18, "pos_emb_shape": (8, 16, 16), "model_dim": 1024,
+        "num_spatial_layers": 24, "num_temporal_layers": 4, "num_heads": 16, "mlp_dim": 4096,
+        "atten_logit_cap": 50.0, "norm_policy": "pre"},
+    "videoprism_lvt_public_v1_base": {
+        "patch_size": 18, "pos_emb_shape": (16, 16, 16), "num_spatial_layers": 12,
+        "num_temporal_layers": 4, "mlp_dim": 3072, "num_auxiliary_layers": 2,
+        "vocabulary_size": 32000, "enable_causal_atten": True, "num_unimodal_layers": 12,
+        "norm_policy": "pre", "model_dim": 768, "num_heads": 12, "atten_logit_cap": 50.0},
+    "videoprism_lvt_public_v1_large": {
+        "patch_size": 18, "pos_emb_shape": (8, 16, 16), "num_spatial_layers": 24,
+        "num_temporal_layers": 4, "mlp_dim": 4096, "num_auxiliary_layers": 2,
+        "vocabulary_size": 32000, "enable_causal_atten": True, "num_unimodal_layers": 12,
+        "norm_policy": "pre", "model_dim": 1024, "num_heads": 16, "atten_logit_cap": 50.0},
+}
+
+
+def get_model_config(model_name: str) -> dict:
+    """models_mlx.py:72-88."""
+    if model_name not in MODEL_CONFIGS:
+        available = ", ".join(MODEL_CONFIGS.keys())
+        raise ValueError(f"Model '{model_name}' not found. Available models: {available}")
+    return MODEL_CONFIGS[model_name].copy()
+
+
+def _resolve(model_name: str, weights_path) -> Path:
+    if weights_path is None:
+        weights_dir = Path("weights")
+        weights_path = weights_dir / f"{model_name}_mlx.safetensors"
+        if not weights_path.exists():
+            weights_path = weights_dir / f"{model_name}_mlx.npz"
+    else:
+        weights_path = Path(weights_path)
+    if not weights_path.exists():
+        raise FileNotFoundError(f"Weights not found at {weights_path}. "
+                                f"Please run: python convert_weights.py")
+    return weights_path
+
+
+def load_weights_from_file(filepath: str) -> dict:
+    """models_mlx.py:297-316 — flat {name: array}."""
+    filepath = Path(filepath)
+    if not filepath.exists():
+        raise FileNotFoundError(f"File not found: {filepath}")
+    if filepath.suffix == ".safetensors":
+        from safetensors.numpy import load_file
+        return dict(load_file(str(filepath)))
+    if filepath.suffix == ".npz":
+        return dict(np.load(str(filepath), allow_pickle=False))
+    raise ValueError(f"Unsupported file format: {filepath.suffix}")
+
+
+class VideoEncoder:
+    """Callable wrapper: `model(video, return_intermediate=False, frame_paddings=None)`."""
+
+    def __init__(self, config: dict, variables: dict, fprop_dtype=None):
+        cfg = {k: v for k, v in config.items() if k != "norm_policy"}
+        self.encoder = encoders.FactorizedEncoder(norm_policy=config.get("norm_policy", "pre"),
+                                                  fprop_dtype=fprop_dtype, **cfg)
+        self.variables = variables
+
+    def __call__(self, inputs, return_intermediate=False, frame_paddings=None):
+        return self.encoder.apply(self.variables, inputs, train=False,
+                                  return_intermediate=return_intermediate,
+                                  frame_paddings=frame_paddings)
+
+
+def load_video_encoder(model_name: str, weights_path: str = None, fprop_dtype=None) -> VideoEncoder:
+    """models_mlx.py:146-210."""
+    config = get_model_config(model_name)
+    if "lvt" in model_name:
+        raise ValueError(
+            f"Model '{model_name}' is a video-text model. Use load_model() instead, or use a "
+            f"video-only model like 'videoprism_public_v1_base' or 'videoprism_public_v1_large'")
+    path = _resolve(model_name, weights_path)
+    flat = load_weights_from_file(str(path))
+    canonical = params_lib.canonical_params(flat)
+    # drop an 'params/' or 'vision_encoder/' prefix if the file carries one
+    canonical = {k.split("vision_encoder/", 1)[-1]: v for k, v in canonical.items()}
+    return VideoEncoder(config, {"params": utils.recover_tree(list(canonical), list(canonical.values()))},
+                        fprop_dtype=fprop_dtype)
+
+
+def load_model(model_name: str, weights_path: str = None):
+    """models_mlx.py:91-143 (video-text CLIP): not yet available on MI355X."""
+    get_model_config(model_name)
+    raise NotImplementedError("LvT video-text models are not implemented on MI355X yet "
+                              "(SURVEY.md §8(f) f1)")
+
+
+def load_classifier(model_name: str, num_classes: int, weights_path: str = None):
+    """models_mlx.py:213-294: FactorizedVideoClassifier is out of scope."""
+    get_model_config(model_name)
+    raise NotImplementedError("FactorizedVideoClassifier is out of scope for this build")
