@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""VideoPrism-Base bf16 forward throughput on MI355X (BASELINE.json metric/configs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one forward of the `videoprism_public_v1_base` FactorizedEncoder (bf16, random-init
+weights of the real architecture) over B=32 synthetic clips [32,16,288,288,3] uniform[0,1)
+already resident in HBM (configs[1]); for N>1 every rank runs its own 32 clips (weak
+scaling, configs[3]: B=32*N) and the step includes the RCCL all-gather of the pooled,
+L2-normalised clip embeddings.  value = clips processed by all ranks / max-over-ranks time.
+
+Also reported (one JSON line on rank 0):
+  roofline     the dominant kernel's algorithmic FLOP (or byte) rate, from HIP events recorded
+               on its launch stream inside the timed region, against the MI355X dense peak
+  cpu_baseline the NumPy oracle (oracle/, fp32) on one clip on this host's cores (rank 0, N=1)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip parameters)
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (same table)
+
+
+def gflop_per_clip(cfg: dict, T: int = 16, N: int = 256) -> float:
+    """Algorithmic GFLOP per clip (2 flop/MAC): GEMMs + attention + patch embed."""
+    D, F = cfg["model_dim"], cfg["mlp_dim"]
+    Ls, Lt = cfg["num_spatial_layers"], cfg["num_temporal_layers"]
+    P = cfg["patch_size"]
+    tok = T * N
+    gemm = (8 * D * D + 4 * D * F) * tok * (Ls + Lt)
+    sp_att = 4 * N * N * D * T * Ls
+    tp_att = 4 * T * T * D * N * Lt
+    patch = 2 * P * P * 3 * D * tok
+    return (gemm + sp_att + tp_att + patch) / 1e9
+
+
+def cpu_baseline(cfg, variables) -> dict:
+    """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip — a reported baseline only."""
+    import numpy as np
+    from threadpoolctl import threadpool_info
+
+    from oracle import videoprism_oracle as orc
+    rng = np.random.default_rng(0)
+    video = rng.random((1, 16, 288, 288, 3), dtype=np.float32)
+    t0 = time.perf_counter()
+    orc.factorized_encoder(variables["params"], video, cfg, mode="f32")
+    dt = time.perf_counter() - t0
+    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    return {"value": round(1.0 / dt, 5), "unit": "clips/s", "cores": int(threads), "kind": "port",
+            "sample": f"1 clip [1,16,288,288,3], full videoprism_public_v1_base forward, NumPy fp32 "
+                      f"oracle (oracle/videoprism_oracle.py), {dt:.1f} s; host has "
+                      f"{len(os.sched_getaffinity(0))} schedulable CPUs"}
+
+
+def load_traffic(path: str, kernel: str):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    k = t.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k.get("hbm_bytes_per_launch"), t.get("source")
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    import torch
+
+    from videoprism import _native, distributed, models, params
+
+    rank, local_rank, world = distributed.init("nccl")
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device(f"cuda:{local_rank}")
+
+    name = "videoprism_public_v1_base"
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    variables = params.synthetic_params(cfg, seed=0)
+    model = models.get_model(name, fprop_dtype=torch.bfloat16)
+    eng = model.engine(variables, local_rank)
+
+    B, T = args.batch, args.frames
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev).to(torch.bfloat16)
+    out = torch.empty((B, T * 256, cfg["model_dim"]), dtype=torch.bfloat16, device=dev)
+    gather = world > 1 and not args.no_allgather
+
+    def step():
+        eng.forward(video, out=out)
+        if gather:
+            pooled = _native.op_pool_l2(out)
+            distributed.all_gather_rows(pooled, world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    launches_per_fwd = 3 + 7 * (cfg["num_spatial_layers"] + cfg["num_temporal_layers"]) + 2
+    if not args.no_profile:
+        eng.profile_enable(args.steps * launches_per_fwd + 16)
+    distributed.barrier(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    distributed.barrier(dev)
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dev)
+    prof = eng.profile_read() if not args.no_profile else {}
+
+    clips = world * B * args.steps
+    value = clips / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    gpc = gflop_per_clip(cfg, T)
+
+    roofline = None
+    kernel_ms = {}
+    if prof:
+        kernel_ms = {k: round(v["ms"] / args.steps, 4) for k, v in
+                     sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+        dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+        avg_s = dom["ms"] / dom["launches"] / 1e3
+        traffic, tsrc = load_traffic(args.traffic, dom_name)
+        if dom["flops"] > 0:
+            ach = dom["flops"] / dom["launches"] / avg_s / 1e12
+            roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                        "traffic": traffic}
+        else:
+            ach = dom["bytes"] / dom["launches"] / avg_s / 1e9
+            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                        "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic}
+        roofline.update({"kernel": dom_name, "launches": int(dom["launches"]),
+                         "avg_launch_us": round(avg_s * 1e6, 2),
+                         "algorithmic_per_launch": dom["flops"] / dom["launches"] if dom["flops"]
+                         else dom["bytes"] / dom["launches"], "traffic_source": tsrc})
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, variables)
+
+    if rank == 0:
+        line = {
+            "metric": "clips/sec (16x288x288) VideoPrism-Base fwd; % MFMA peak",
+            "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic uniform[0,1) clips generated on device; random-init weights of the "
+                    "real architecture (no checkpoint offline)",
+            "config": {"workload": f"{name} bf16 forward, B={B} clips/GPU x {world} GPU, "
+                                   f"{T}x288x288x3" + (", RCCL all-gather of pooled embeddings"
+                                                       if gather else ""),
+                       "model": name, "global_batch": B * world, "frames": T,
+                       "parallelism": f"dp{world} (batch-sharded clips)"},
+            "mfma_util_whole_forward": round(value / world * gpc / 1e3 / PEAK_BF16_TFLOPS, 4),
+            "gflop_per_clip": round(gpc, 2),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms_per_step": kernel_ms,
+        }
+        print(json.dumps(line), flush=True)
+
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

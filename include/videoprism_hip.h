@@ -99,11 +99,22 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
                int64_t W, const float* frame_paddings, void* out, int out_dtype,
                void* spatial_out, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---------------- HIP-event profiler (bench.py's live per-kernel timing) ----------------
+ * vp_profile_enable(h, n): the next n kernel launches of vp_forward are bracketed by
+ * hipEventRecord on the launch stream (0 disables).  vp_profile_read syncs on the last event
+ * and returns, per kernel class (vp_profile_class_name), the summed milliseconds, algorithmic
+ * FLOPs and bytes and the launch count since the previous read, then resets. */
+int vp_profile_enable(vp_handle* h, int capacity);
+int vp_profile_read(vp_handle* h, int nclass, double* ms, double* flops, double* bytes,
+                    int64_t* launches);
+int vp_profile_class_count(void);
+int vp_profile_class_name(int cls, const char** name);
+
 /* ---------------- op-level entry points (kernel parity tests, benches) ---------------- */
 
 /* C[M,N] = A[M,K].W[N,K]^T + bias with epilogue:
  *   0 store (out dtype = precision), 1 GELU(erf) [* (1-rowpad)], 2 out_f32 = resid + (.)*(1-rowpad),
- *   3 out_f32 = (.) + pos[m % pos_rows].   precision VP_BF16: A,W bf16; VP_F32: A,W fp32.
+ *   3 out_f32 = (.) + pos[m % pos_rows], 4 = 2 (separate kernel symbol used for ffn_layer2).   precision VP_BF16: A,W bf16; VP_F32: A,W fp32.
  * Replaces layers.py:273-313 (Dense) and :433-499 (einsum projections). */
 int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const void* W, int64_t ldw,
                int64_t M, int64_t N, int64_t K, void* out, int64_t ldo, const float* bias,

@@ -46,7 +46,7 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& ep, int N, int m, 
     }
     uint2 o = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
     *reinterpret_cast<uint2*>(static_cast<bf16_t*>(ep.out) + (int64_t)m * ep.ldo + n) = o;
-  } else if constexpr (EPI == EPI_RESID_F32) {
+  } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
     if (ep.rowpad) {
       const float keep = 1.0f - ep.rowpad[m];
       v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
@@ -183,6 +183,7 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
     case EPI_GELU_BF16: return launch_one<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_F32: return launch_one<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_F32: return launch_one<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN: return launch_one<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

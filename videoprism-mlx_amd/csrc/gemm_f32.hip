@@ -29,7 +29,7 @@ __device__ __forceinline__ void epi_f32(const EpiArgs& ep, int N, int m, int n, 
       v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
     }
     *reinterpret_cast<float4*>(out) = make_float4(v0, v1, v2, v3);
-  } else if constexpr (EPI == EPI_RESID_F32) {
+  } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
     if (ep.rowpad) {
       const float keep = 1.0f - ep.rowpad[m];
       v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
@@ -147,6 +147,7 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
     case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_F32: return launch<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_F32: return launch<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN: return launch<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

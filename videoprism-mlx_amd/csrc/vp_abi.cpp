@@ -88,6 +88,22 @@ struct LayerW {  // one transformer layer, packed
 
 constexpr int kMaxT = 32;
 
+enum ProfClass {
+  PC_PATCHIFY = 0, PC_GEMM_PATCH, PC_LAYERNORM, PC_GEMM_QKV, PC_ATTN_SPATIAL, PC_ATTN_TEMPORAL,
+  PC_GEMM_POST, PC_GEMM_FFN1, PC_GEMM_FFN2, PC_MISC, PC_COUNT
+};
+const char* kProfNames[PC_COUNT] = {"patchify", "gemm_patch_embed", "layernorm", "gemm_qkv",
+                                    "attention_spatial", "attention_temporal", "gemm_post",
+                                    "gemm_ffn1_gelu", "gemm_ffn2", "misc"};
+
+// HIP-event profiler: start/stop events around each launch on the launch stream.
+struct Profiler {
+  int cap = 0, used = 0;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> cls;
+  std::vector<double> flops, bytes;
+};
+
 }  // namespace
 
 struct vp_handle {
@@ -106,6 +122,7 @@ struct vp_handle {
   float* temporal_pos = nullptr;   // [kMaxT+1][kMaxT][D]: table for T at offset T*kMaxT*D
   std::vector<LayerW> spatial, temporal;
   float *sln_g = nullptr, *sln_b = nullptr, *tln_g = nullptr, *tln_b = nullptr;
+  Profiler prof;
 };
 
 namespace {
@@ -335,6 +352,7 @@ int vp_destroy(vp_handle* h) {
   if (!h) return VP_OK;
   hipSetDevice(h->device);
   for (auto& a : h->allocs) hipFree(a.p);
+  for (auto& e : h->prof.ev) hipEventDestroy(e);
   delete h;
   return VP_OK;
 }
@@ -486,28 +504,53 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   };
   const char* ge = bf ? gemm_bf16_check(M, 3 * D, D, D, D) : gemm_f32_check(M, 3 * D, D);
   if (ge) return fail(VP_ENOTSUP, ge);
+  // profiled launch: records events around `fn` when vp_profile_enable() is active
+  Profiler& pf = h->prof;
+  auto rec = [&](int cls, double flops, double bytes, auto&& fn) -> hipError_t {
+    if (pf.used >= pf.cap) return fn();
+    const int i = pf.used++;
+    hipError_t e = hipEventRecord(pf.ev[2 * i], s);
+    if (e != hipSuccess) return e;
+    e = fn();
+    if (e != hipSuccess) return e;
+    pf.cls[i] = cls; pf.flops[i] = flops; pf.bytes[i] = bytes;
+    return hipEventRecord(pf.ev[2 * i + 1], s);
+  };
+  const double dM = M, dD = D, dF = F, dE = (double)es;
+  auto gbytes = [&](double K, double N, double outb, double resid) {  // algorithmic GEMM bytes
+    return dM * K * dE + N * K * dE + dM * N * outb + dM * N * resid;
+  };
 
   // 1. tokenisation + patch projection + spatial pos-emb (encoders.py:436-514)
-  VP_HIP(patchify(video, in_dtype == VP_BF16, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s));
-  VP_HIP(gemm(EPI_POS_F32, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr, h->spatial_pos, Nsp, nullptr));
+  const double kreal = (double)P_ * P_ * 3;
+  VP_HIP(rec(PC_PATCHIFY, 0.0, dM * kreal * (in_dtype == VP_BF16 ? 2 : 4) + dM * h->kpad * dE, [&] {
+    return patchify(video, in_dtype == VP_BF16, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
+  VP_HIP(rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, 4, 0), [&] {
+    return gemm(EPI_POS_F32, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr, h->spatial_pos, Nsp, nullptr); }));
+  const double ln_bytes = dM * dD * 4 + dM * dD * dE;
 
   auto run_stack = [&](std::vector<LayerW>& layers, float* xs, int num_seq, int S,
                        const float* pad) -> int {
+    const int acls = num_seq == (int)(B * T) ? PC_ATTN_SPATIAL : PC_ATTN_TEMPORAL;
+    const double aflops = 4.0 * num_seq * (double)S * S * dD;
+    const double abytes = dM * 3 * dD * dE + dM * dD * dE;
     for (auto& lw : layers) {
-      VP_HIP(layernorm(xs, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s));
-      VP_HIP(gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr));
-      if (bf) {
-        if (S == 256)
-          VP_HIP(attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, c.atten_logit_cap, pad, s));
-        else
-          VP_HIP(attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s));
-      } else {
-        VP_HIP(attention_f32((const float*)big, (float*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s));
-      }
-      VP_HIP(gemm(EPI_RESID_F32, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1, nullptr));
-      VP_HIP(layernorm(xs, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s));
-      VP_HIP(gemm(EPI_GELU_BF16, hb, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad));
-      VP_HIP(gemm(EPI_RESID_F32, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1, pad));
+      VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
+        return layernorm(xs, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
+      VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
+        return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
+      VP_HIP(rec(acls, aflops, abytes, [&] {
+        if (!bf) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s);
+        if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, c.atten_logit_cap, pad, s);
+        return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s); }));
+      VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, 4, 4), [&] {
+        return gemm(EPI_RESID_F32, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1, nullptr); }));
+      VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
+        return layernorm(xs, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
+      VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
+        return gemm(EPI_GELU_BF16, hb, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad); }));
+      VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, 4, 4), [&] {
+        return gemm(EPI_RESID_FFN, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1, pad); }));
     }
     return VP_OK;
   };
@@ -515,16 +558,65 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   if ((rc = run_stack(h->spatial, x, (int)(B * T), Nsp, pad_btn))) return rc;
   // 3. spatial_ln (+ optional spatial_features), transpose to (b n) t, + temporal pos-emb
   if (spatial_out)
-    VP_HIP(layernorm(x, M, D, h->sln_g, h->sln_b, spatial_out, out_dtype == VP_BF16, PERM_NONE, 1, 1, nullptr, s));
+    VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * 4 + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
+      return layernorm(x, M, D, h->sln_g, h->sln_b, spatial_out, out_dtype == VP_BF16, PERM_NONE, 1, 1, nullptr, s); }));
   const float* tpos = h->temporal_pos + (size_t)T * kMaxT * D;
-  VP_HIP(layernorm(x, M, D, h->sln_g, h->sln_b, x2, 0, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s));
+  VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * 8, [&] {
+    return layernorm(x, M, D, h->sln_g, h->sln_b, x2, 0, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s); }));
   // 4. temporal encoder over (b n) sequences of T tokens
   if ((rc = run_stack(h->temporal, x2, (int)(B * Nsp), (int)T, pad_bnt))) return rc;
   // 5. temporal_ln and '(bn)td->b(tn)d'
-  VP_HIP(layernorm(x2, M, D, h->tln_g, h->tln_b, out, out_dtype == VP_BF16, PERM_BNT_TO_BTN, (int)T, Nsp, nullptr, s));
+  VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * 4 + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
+    return layernorm(x2, M, D, h->tln_g, h->tln_b, out, out_dtype == VP_BF16, PERM_BNT_TO_BTN, (int)T, Nsp, nullptr, s); }));
   (void)es;
   return VP_OK;
 }
+
+// ----------------------------------- profiling ----------------------------------------
+
+int vp_profile_enable(vp_handle* h, int capacity) {
+  if (!h || capacity < 0) return fail(VP_EINVAL, "bad argument");
+  VP_HIP(hipSetDevice(h->device));
+  Profiler& p = h->prof;
+  for (auto& e : p.ev) hipEventDestroy(e);
+  p.ev.clear();
+  p.cap = 0;
+  p.used = 0;
+  p.ev.resize((size_t)capacity * 2);
+  for (auto& e : p.ev) VP_HIP(hipEventCreate(&e));
+  p.cls.assign(capacity, PC_MISC);
+  p.flops.assign(capacity, 0.0);
+  p.bytes.assign(capacity, 0.0);
+  p.cap = capacity;
+  return VP_OK;
+}
+
+int vp_profile_read(vp_handle* h, int nclass, double* ms, double* flops, double* bytes,
+                    int64_t* launches) {
+  if (!h || nclass < PC_COUNT || !ms || !flops || !bytes || !launches)
+    return fail(VP_EINVAL, "bad argument");
+  for (int c = 0; c < nclass; ++c) { ms[c] = 0; flops[c] = 0; bytes[c] = 0; launches[c] = 0; }
+  Profiler& p = h->prof;
+  if (p.used > 0) VP_HIP(hipEventSynchronize(p.ev[2 * p.used - 1]));
+  for (int i = 0; i < p.used; ++i) {
+    float t = 0.f;
+    VP_HIP(hipEventElapsedTime(&t, p.ev[2 * i], p.ev[2 * i + 1]));
+    ms[p.cls[i]] += t;
+    flops[p.cls[i]] += p.flops[i];
+    bytes[p.cls[i]] += p.bytes[i];
+    launches[p.cls[i]] += 1;
+  }
+  p.used = 0;
+  return VP_OK;
+}
+
+int vp_profile_class_name(int cls, const char** name) {
+  if (cls < 0 || cls >= PC_COUNT || !name) return fail(VP_EINVAL, "bad class");
+  *name = kProfNames[cls];
+  return VP_OK;
+}
+
+int vp_profile_class_count(void) { return PC_COUNT; }
 
 // ----------------------------------- op level -----------------------------------------
 
@@ -534,8 +626,8 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
                const float* rowpad, void* stream) {
   using namespace vp;
   if (!A || !W || !out || !bias) return fail(VP_EINVAL, "null argument");
-  if (epilogue < 0 || epilogue > 3) return fail(VP_EINVAL, "bad epilogue");
-  if (epilogue == EPI_RESID_F32 && !resid) return fail(VP_EINVAL, "resid required");
+  if (epilogue < 0 || epilogue > 4) return fail(VP_EINVAL, "bad epilogue");
+  if ((epilogue == EPI_RESID_F32 || epilogue == EPI_RESID_FFN) && !resid) return fail(VP_EINVAL, "resid required");
   if (epilogue == EPI_POS_F32 && (!pos || pos_rows < 1)) return fail(VP_EINVAL, "pos required");
   EpiArgs ep;
   ep.out = out; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldr;

@@ -13,6 +13,7 @@ enum Epilogue {
   EPI_GELU_BF16 = 1,  // out_bf16 = gelu(acc + bias) * (1 - rowpad)  (ffn_layer1)
   EPI_RESID_F32 = 2,  // out_f32  = resid + (acc + bias) * (1 - rowpad)   (post, ffn_layer2)
   EPI_POS_F32 = 3,    // out_f32  = acc + bias + pos[m % pos_rows]   (patch_projection + pos emb)
+  EPI_RESID_FFN = 4,  // = EPI_RESID_F32, separate kernel symbol for ffn_layer2 (profiling)
 };
 
 struct EpiArgs {

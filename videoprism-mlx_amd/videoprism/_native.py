@@ -17,7 +17,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
 VP_OK, VP_EINVAL, VP_ENOMEM, VP_EHIP, VP_ESTATE, VP_ENOTSUP = range(6)
 VP_F32, VP_BF16 = 0, 1
 
-EPI_STORE, EPI_GELU, EPI_RESID, EPI_POS = 0, 1, 2, 3
+EPI_STORE, EPI_GELU, EPI_RESID, EPI_POS, EPI_RESID_FFN = 0, 1, 2, 3, 4
 PERM_NONE, PERM_BTN_TO_BNT, PERM_BNT_TO_BTN = 0, 1, 2
 
 
@@ -60,6 +60,11 @@ _SIGNATURES = {
     "vp_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "vp_forward": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "vp_profile_enable": (c_int, [c_void_p, c_int]),
+    "vp_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
+                                POINTER(ctypes.c_double), POINTER(c_int64)]),
+    "vp_profile_class_count": (c_int, []),
+    "vp_profile_class_name": (c_int, [c_int, POINTER(c_char_p)]),
     "vp_op_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64,
                            c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
                            c_int64, c_void_p, c_void_p]),

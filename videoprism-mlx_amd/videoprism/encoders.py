@@ -74,6 +74,26 @@ class Engine:
             _native._lib.vp_destroy(h)
             self._h = None
 
+    # -- live per-kernel timing (HIP events on the launch stream, vp_profile_*) ---------
+    def profile_enable(self, capacity: int) -> None:
+        _native.call("vp_profile_enable", self._h, int(capacity))
+
+    def profile_read(self) -> dict:
+        lib = _native.load()
+        n = lib.vp_profile_class_count()
+        ms = (ctypes.c_double * n)()
+        fl = (ctypes.c_double * n)()
+        by = (ctypes.c_double * n)()
+        la = (ctypes.c_int64 * n)()
+        _native.call("vp_profile_read", self._h, n, ms, fl, by, la)
+        out = {}
+        for i in range(n):
+            name = ctypes.c_char_p()
+            _native.call("vp_profile_class_name", i, ctypes.byref(name))
+            if la[i]:
+                out[name.value.decode()] = dict(ms=ms[i], flops=fl[i], bytes=by[i], launches=la[i])
+        return out
+
     def workspace(self, B, T, H, W):
         torch = _torch()
         n = ctypes.c_size_t()
