@@ -1,0 +1,85 @@
+"""Generates the committed golden fixtures from the NumPy oracle (oracle/videoprism_oracle.py).
+
+PARITY UNPINNED by the reference: its tests hold no value-level vectors for this path
+(SURVEY.md §8(c)), JAX is not installed here, so these fixtures pin the oracle against
+future drift and give the GPU tests fixed vectors; their cross-check is the independent
+torch restatement (tests/torch_restatement.py) and the structural pins of the reference
+tests.  Run:  python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
+
+from oracle import videoprism_oracle as orc  # noqa: E402
+from videoprism import models, params  # noqa: E402
+
+# encoders_test.py:130,145-156 — the reference's own tiny FactorizedEncoder
+TINY = dict(patch_size=4, pos_emb_shape=(16, 16, 16), model_dim=8, num_spatial_layers=2,
+            num_temporal_layers=2, num_heads=2, mlp_dim=4, atten_logit_cap=50.0)
+
+
+def g1_tiny():
+    var = params.synthetic_params(TINY, seed=0)
+    flat = params.flatten(var["params"])
+    x = np.random.default_rng(0).normal(0.0, 0.1, (1, 4, 16, 16, 3)).astype(np.float32)
+    emb, out = orc.factorized_encoder(var["params"], x, TINY, "f64", return_intermediate=True)
+    fp = np.zeros((1, 4), np.float32)
+    fp[:, 2:] = 1.0  # encoders_test.py:138-142
+    emb_p, _ = orc.factorized_encoder(var["params"], x, TINY, "f64", frame_paddings=fp)
+    arrays = {f"param/{k}": v for k, v in flat.items()}
+    arrays.update(inputs=x, frame_paddings=fp, embeddings=emb, spatial_features=out["spatial_features"],
+                  embeddings_padded=emb_p)
+    np.savez_compressed(os.path.join(HERE, "g1_tiny.npz"), **arrays)
+
+
+def g2_base_dims():
+    cfg = dict(models.CONFIGS["videoprism_v1_base"])
+    cfg.update(num_spatial_layers=2, num_temporal_layers=1)
+    var = params.synthetic_params(cfg, seed=1)
+    flat = params.flatten(var["params"])
+    x = np.random.default_rng(3).random((1, 2, 288, 288, 3), dtype=np.float32)
+    emb, _ = orc.factorized_encoder(var["params"], x, cfg, "f64")
+    idx = np.arange(0, emb.size, 997)
+    np.savez_compressed(
+        os.path.join(HERE, "g2_base_dims.npz"),
+        param_names=np.array(sorted(flat)),
+        param_sums=np.array([float(np.sum(flat[k], dtype=np.float64)) for k in sorted(flat)]),
+        param_heads=np.stack([flat[k].ravel()[:4] for k in sorted(flat)]),
+        input_seed=np.array(3), param_seed=np.array(1), sample_index=idx,
+        sample_values=emb.ravel()[idx], row_sums=emb.sum(axis=-1).ravel(),
+        shape=np.array(emb.shape))
+
+
+def g4_ops():
+    rng = np.random.default_rng(4)
+    nm = orc.Numerics("f64")
+    x = rng.normal(1.0, 3.0, (5, 768))
+    sc, bi = rng.normal(0, 0.1, 768), rng.normal(0, 0.1, 768)
+    g = np.linspace(-6, 6, 97)
+    q, k, v = rng.normal(0, 1, (3, 2, 16, 64))
+    q = q * 4.0
+    kp = np.zeros((2, 16))
+    kp[1, ::3] = 1
+    img = rng.random((2, 6, 6, 3))
+    np.savez_compressed(
+        os.path.join(HERE, "g4_ops.npz"),
+        ln_x=x, ln_scale=sc, ln_bias=bi, ln_out=orc.layer_norm(x, sc, bi, nm),
+        gelu_x=g, gelu_y=orc.gelu(g),
+        att_q=q, att_k=k, att_v=v, att_key_pad=kp,
+        att_out=orc.capped_softmax_attention(q, k, v, 50.0, kp),
+        patch_img=img, patch_out=orc.image_to_patch(img, 3),
+        resize_up_8_16=orc._resize_weights(8, 16), resize_down_16_4=orc._resize_weights(16, 4))
+
+
+if __name__ == "__main__":
+    g1_tiny()
+    g2_base_dims()
+    g4_ops()
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -1,0 +1,123 @@
+"""Second, independent CPU restatement of the FactorizedEncoder forward in plain PyTorch
+(fp64) — test infrastructure used only to cross-check the NumPy oracle.
+
+Written from the reference's module semantics (encoders.py:411-580, layers.py:208-872)
+with torch primitives (F.layer_norm, torch.erf, torch.softmax, einsum) instead of the
+oracle's NumPy code, so that a shared misreading would have to be made twice.
+"""
+
+import torch
+import torch.nn.functional as F
+
+
+def _t(x):
+    return torch.as_tensor(x, dtype=torch.float64)
+
+
+def _ln(x, p):
+    d = x.shape[-1]
+    return F.layer_norm(x, (d,), weight=_t(p["scale"]) + 1.0, bias=_t(p["bias"]), eps=1e-6)
+
+
+def _stack(x, st, L, heads, cap, paddings):
+    xl = st["x_layers"]
+    B, S, D = x.shape
+    dh = D // heads
+    if paddings is not None:
+        pad = torch.as_tensor(paddings, dtype=torch.float64)
+    else:
+        pad = torch.zeros(B, S, dtype=torch.float64)
+    masked = pad[:, None, None, :] > 0.5
+    all_masked = masked.all(dim=-1, keepdim=True)
+    for i in range(L):
+        sa = xl["self_attention"]
+        h = F.layer_norm(x, (D,), weight=_t(xl["layer_norm"]["scale"][i]) + 1.0,
+                         bias=_t(xl["layer_norm"]["bias"][i]), eps=1e-6)
+        q = torch.einsum("bsd,dnh->bsnh", h, _t(sa["query"]["w"][i])) + _t(sa["query"]["b"][i])
+        k = torch.einsum("bsd,dnh->bsnh", h, _t(sa["key"]["w"][i])) + _t(sa["key"]["b"][i])
+        v = torch.einsum("bsd,dnh->bsnh", h, _t(sa["value"]["w"][i])) + _t(sa["value"]["b"][i])
+        q = q / dh ** 0.5
+        logits = torch.einsum("btnh,bsnh->bnts", q, k)
+        logits = cap * torch.tanh(logits / cap)
+        # masked keys drop out; a row whose keys are all masked attends uniformly
+        logits = torch.where(masked & ~all_masked, torch.full_like(logits, -1e300), logits)
+        logits = torch.where(all_masked.expand_as(logits), torch.zeros_like(logits), logits)
+        probs = torch.softmax(logits, dim=-1)
+        enc = torch.einsum("bnts,bsnh->btnh", probs, v)
+        att = torch.einsum("btnh,dnh->btd", enc, _t(sa["post"]["w"][i])) + _t(sa["post"]["b"][i])
+        x = x + att
+        ff = xl["ff_layer"]
+        y = F.layer_norm(x, (D,), weight=_t(ff["layer_norm"]["scale"][i]) + 1.0,
+                         bias=_t(ff["layer_norm"]["bias"][i]), eps=1e-6)
+        a = y @ _t(ff["ffn_layer1"]["linear"]["kernel"][i]) + _t(ff["ffn_layer1"]["linear"]["bias"][i])
+        a = 0.5 * a * (1.0 + torch.erf(a / 2 ** 0.5))
+        a = a * (1.0 - pad[..., None])
+        o = a @ _t(ff["ffn_layer2"]["linear"]["kernel"][i]) + _t(ff["ffn_layer2"]["linear"]["bias"][i])
+        o = o * (1.0 - pad[..., None])
+        x = x + o
+    return x
+
+
+def _resize(emb, out_len):
+    """jax.image.resize(..., 'bilinear') along axis 0: for upsampling the half-pixel
+    linear interpolation with edge clamp of encoders_mlx.py:104-137; for downsampling a
+    triangle filter stretched by in/out (antialias), each output normalised to sum 1."""
+    n = emb.shape[0]
+    if out_len >= n:
+        coords = (torch.arange(out_len, dtype=torch.float64) + 0.5) * (n / out_len) - 0.5
+        lo = torch.floor(coords)
+        wu = torch.clamp(coords - lo, 0.0, 1.0)
+        li = torch.clamp(lo.long(), 0, n - 1)
+        ui = torch.clamp(lo.long() + 1, 0, n - 1)
+        return emb[li] * (1 - wu)[:, None] + emb[ui] * wu[:, None]
+    ratio = n / out_len
+    centres = (torch.arange(out_len, dtype=torch.float64) + 0.5) * ratio - 0.5
+    src = torch.arange(n, dtype=torch.float64)
+    wts = torch.clamp(1.0 - (src[None, :] - centres[:, None]).abs() / ratio, min=0.0)
+    wts = wts / wts.sum(dim=1, keepdim=True)
+    return wts @ emb
+
+
+def _resize_2d(emb, src_hw, dst_hw):
+    d = emb.shape[-1]
+    e = emb.reshape(src_hw[0], src_hw[1], d)
+    e = _resize(e.reshape(src_hw[0], -1), dst_hw[0]).reshape(dst_hw[0], src_hw[1], d)
+    e = _resize(e.permute(1, 0, 2).reshape(src_hw[1], -1), dst_hw[1])
+    return e.reshape(dst_hw[1], dst_hw[0], d).permute(1, 0, 2).reshape(dst_hw[0] * dst_hw[1], d)
+
+
+def factorized_encoder(params, video, cfg, frame_paddings=None):
+    P, D = cfg["patch_size"], cfg["model_dim"]
+    heads, cap = cfg["num_heads"], cfg["atten_logit_cap"]
+    x = _t(video)
+    b, t, h, w, c = x.shape
+    m, n = h // P, w // P
+    patches = x.reshape(b * t, m, P, n, P, c).permute(0, 1, 3, 2, 4, 5).reshape(b * t, m * n, P * P * c)
+    pp = params["patch_projection"]["linear"]
+    feats = patches @ _t(pp["kernel"]) + _t(pp["bias"])
+    pe = _t(params["spatial_pos_emb"]["emb_var"])
+    src_hw = tuple(cfg["pos_emb_shape"][-2:])
+    pe = pe[: src_hw[0] * src_hw[1]]
+    if src_hw != (m, n):
+        pe = _resize_2d(pe, src_hw, (m, n))
+    feats = feats + pe[None]
+    sp_pad = None
+    tp_pad = None
+    if frame_paddings is not None:
+        fp = _t(frame_paddings)
+        sp_pad = fp.reshape(b * t, 1).expand(b * t, m * n)
+        tp_pad = fp[:, None, :].expand(b, m * n, t).reshape(b * m * n, t)
+    feats = _stack(feats, params["spatial_encoder"]["transformers_stack"], cfg["num_spatial_layers"],
+                   heads, cap, sp_pad)
+    feats = _ln(feats, params["spatial_ln"])
+    spatial = feats.reshape(b, t * m * n, D)
+    feats = feats.reshape(b, t, m * n, D).permute(0, 2, 1, 3).reshape(b * m * n, t, D)
+    temb = _t(params["temporal_pos_emb"]["emb_var"])
+    if temb.shape[0] != t:
+        temb = _resize(temb, t)
+    feats = feats + temb[None]
+    feats = _stack(feats, params["temporal_encoder"]["transformers_stack"], cfg["num_temporal_layers"],
+                   heads, cap, tp_pad)
+    feats = _ln(feats, params["temporal_ln"])
+    out = feats.reshape(b, m * n, t, D).permute(0, 2, 1, 3).reshape(b, t * m * n, D)
+    return out.numpy(), spatial.numpy()

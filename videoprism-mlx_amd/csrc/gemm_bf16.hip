@@ -7,14 +7,26 @@
 //           post projection   (layers.py:736-745) + residual add (:855)
 //           ffn_layer1 + GELU (layers.py:370-393) and ffn_layer2 + residual (:400-425)
 //
-// Tile 256x256x64, 8 waves (2 M x 4 N), each wave 128x64 = 8x4 tiles of
-// v_mfma_f32_16x16x32_bf16.  Operands are staged global->LDS by
-// global_load_lds_dwordx4 (lane-linear LDS image; the bank swizzle is applied to the
-// per-lane SOURCE address and undone on the ds_read_b128), double buffered (128 KiB).
-// The MFMA is issued with W as the "A" operand so that each lane's accumulator
-// holds 4 consecutive N columns of one M row: 16-byte fp32 / 8-byte bf16 stores.
-// Workgroups are remapped so that each XCD walks a contiguous range of output
-// tiles (bijective for any grid size): A panels and W stay in that XCD's L2.
+// Structure (MI355X-specific):
+//  * 256x256 output tile per 512-thread workgroup, 8 waves = 2 (M) x 4 (N), each wave
+//    128x64 = 8x4 accumulators of v_mfma_f32_16x16x32_bf16 (128 acc VGPRs).
+//  * K-tile BK=64 is computed in 4 "phases", one per wave quadrant (qm, qn) of 64x32,
+//    order (0,0) (0,1) (1,1) (1,0): 16 MFMAs per phase.  LDS holds 2 K-tile buffers, each
+//    split in 4 regions A0/A1 (tile rows with qm = 0/1) and B0/B1 (cols with qn = 0/1) of
+//    16 KiB.  A region is restaged by global_load_lds two phases after its last ds_read,
+//    so the only VMEM wait is a counted vmcnt(4) once per K-tile (never vmcnt(0) in
+//    steady state) and LDS reads retire under the barrier wait.
+//  * Each phase = [ds_reads + 2 glds] barrier [lgkmcnt(0) + 16 MFMA] barrier.  Waves 4-7
+//    run one barrier behind waves 0-3, so on every SIMD one wave's MFMAs overlap its
+//    partner's LDS reads and DMA issue.
+//  * LDS images are lane-linear for glds; the bank swizzle chunk ^= (row>>1)&7 is applied
+//    to the per-lane SOURCE address and undone on the ds_read_b128 (conflict-free for the
+//    16x16x32 operand pattern).
+//  * W is the MFMA "A" operand, so each lane's accumulator holds 4 consecutive N columns
+//    of one M row (16-byte fp32 / 8-byte bf16 stores); epilogue loads are batched.
+//  * Persistent grid (one workgroup per CU) with a K-tile stream that runs across tiles,
+//    so the next tile's loads overlap this tile's epilogue; each XCD owns a contiguous
+//    tile chunk (L2 locality for A panels and W).
 #include "vp_common.h"
 #include "vp_kernels.h"
 
@@ -24,79 +36,103 @@ namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int kGemmThreads = 512;
-constexpr int kGemmLds = 2 * (BM + BN) * BK * 2;  // 131072 B
+constexpr int kRegion = 128 * BK * 2;       // 16 KiB
+constexpr int kBuf = 4 * kRegion;           // A0 A1 B0 B1
+constexpr int kGemmLds = 2 * kBuf;          // 131072 B
+enum { RA0 = 0, RA1 = 1, RB0 = 2, RB1 = 3 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-__device__ __forceinline__ bf16x8 lds_frag(const char* base, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ swz(row)) << 4));
+__device__ __forceinline__ bf16x8 lds_frag(const char* region, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(region + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
-template <int EPI>
-__device__ __forceinline__ void epilogue_store(const EpiArgs& ep, int N, int m, int n, float v0,
-                                               float v1, float v2, float v3) {
-  if constexpr (EPI == EPI_BF16) {
-    uint2 o = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-    *reinterpret_cast<uint2*>(static_cast<bf16_t*>(ep.out) + (int64_t)m * ep.ldo + n) = o;
-  } else if constexpr (EPI == EPI_GELU_BF16) {
-    v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-    if (ep.rowpad) {
-      const float keep = 1.0f - ep.rowpad[m];
-      v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
-    }
-    uint2 o = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-    *reinterpret_cast<uint2*>(static_cast<bf16_t*>(ep.out) + (int64_t)m * ep.ldo + n) = o;
-  } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
-    if (ep.rowpad) {
-      const float keep = 1.0f - ep.rowpad[m];
-      v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
-    }
-    const float4 r = *reinterpret_cast<const float4*>(ep.resid + (int64_t)m * ep.ldr + n);
-    *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)m * ep.ldo + n) =
-        make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
-  } else {  // EPI_POS_F32
-    const float4 p =
-        *reinterpret_cast<const float4*>(ep.pos + (int64_t)(m % ep.pos_rows) * N + n);
-    *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)m * ep.ldo + n) =
-        make_float4(v0 + p.x, v1 + p.y, v2 + p.z, v3 + p.w);
-  }
+// A&S 7.1.26 erf (|err| <= 1.5e-7) folded into GELU: 0.5*(x + |x|*erf(|x|/sqrt2)).
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
+  p = fmaf(t, p, 1.421413741f);
+  p = fmaf(t, p, -0.284496736f);
+  p = fmaf(t, p, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(x * x * (-0.5f * 1.4426950408889634f));
+  const float erf_abs = fmaf(-p, e, 1.0f);
+  return 0.5f * fmaf(ax, erf_abs, x);
 }
 
-template <int EPI>
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// Persistent: grid = min(tiles, CUs).  The 8 XCDs each own a contiguous chunk of the
+// (tm, tn) tile range (tn fastest) and their workgroups sweep it together, so A panels and
+// W stay in that XCD's L2.  The K-tile stream is global over a workgroup's tiles: the
+// glds of the next tile's first K-tiles are issued during the last K-tiles of the current
+// one, and its epilogue runs while they are in flight (no per-tile pipeline drain).
+// DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 1 = no glds in
+// the K loop, 2 = no ds_reads in the K loop, 4 = no barriers in the K loop, 8 = glds issued
+// but no vmcnt wait in the K loop.
+template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, EpiArgs ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = N / BN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int m0 = (wgid / tilesN) * BM, n0 = (wgid % tilesN) * BN;
+  const int T = (M / BM) * tilesN;
+  const int G = gridDim.x;
+  const int b = blockIdx.x;
+  int first, stride, count;
+  if ((G & 7) == 0) {
+    const int xcd = b & 7, li = b >> 3, nx = G >> 3;
+    const int lo = (int)(((int64_t)xcd * T) >> 3), hi = (int)(((int64_t)(xcd + 1) * T) >> 3);
+    first = lo + li;
+    stride = nx;
+    count = first < hi ? (hi - first + nx - 1) / nx : 0;
+  } else {
+    first = b;
+    stride = G;
+    count = b < T ? (T - b + G - 1) / G : 0;
+  }
+  if (count == 0) return;  // uniform over the workgroup
   const int lane = threadIdx.x & 63;
   const int w = wave_id();
   const int wm = w >> 2, wn = w & 3;
+  const int nk = K / BK;
+  const int total = count * nk;
 
-  // per-lane source rows/chunks of this wave's 4 glds pieces (8 rows x 128 B each)
-  const int srow = lane >> 3;
-  const bf16_t* srcA[4];
-  const bf16_t* srcB[4];
+  // per-lane element offsets of this wave's 2 glds pieces per region (tile-relative):
+  // region q of A holds tile rows (rl>>6)*128 + q*64 + (rl&63); of B tile cols (rl>>5)*64 +
+  // q*32 + (rl&31); chunk swizzle c = (lane&7) ^ swz(rl) applied to the source.
+  int64_t offA[2][2], offB[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rr = (w * 4 + i) * 8 + srow;
-    const int c = (lane & 7) ^ swz(rr);
-    srcA[i] = A + (int64_t)(m0 + rr) * lda + c * 8;
-    srcB[i] = W + (int64_t)(n0 + rr) * ldw + c * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-    char* baseA = smem + buf * 65536;
-    char* baseB = baseA + 32768;
+  for (int i = 0; i < 2; ++i) {
+    const int rl = (w * 2 + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz(rl);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int piece = (w * 4 + i) * 1024;
-      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(srcA[i] + k0), VP_LDS_PTR(baseA + piece), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(srcB[i] + k0), VP_LDS_PTR(baseB + piece), 16, 0, 0);
+    for (int qq = 0; qq < 2; ++qq) {
+      offA[qq][i] = (int64_t)(((rl >> 6) << 7) + qq * 64 + (rl & 63)) * lda + c * 8;
+      offB[qq][i] = (int64_t)(((rl >> 5) << 6) + qq * 32 + (rl & 31)) * ldw + c * 8;
     }
+  }
+  auto tile_of = [&](int g, int& tm, int& tn, int& kt) {
+    const int j = g / nk;
+    kt = g - j * nk;
+    const int tile = first + j * stride;
+    tm = tile / tilesN;
+    tn = tile - tm * tilesN;
+  };
+  auto stage = [&](int region, int g) {
+    if constexpr (DIAG & 1) { if (g > 1) return; }
+    int tm, tn, kt;
+    tile_of(g, tm, tn, kt);
+    char* dst = smem + (g & 1) * kBuf + region * kRegion + w * 2048;
+    const bf16_t* base = region < 2 ? A + (int64_t)tm * BM * lda + kt * BK
+                                    : W + (int64_t)tn * BN * ldw + kt * BK;
+    const int64_t o0 = region == RA0 ? offA[0][0] : region == RA1 ? offA[1][0]
+                     : region == RB0 ? offB[0][0] : offB[1][0];
+    const int64_t o1 = region == RA0 ? offA[0][1] : region == RA1 ? offA[1][1]
+                     : region == RB0 ? offB[0][1] : offB[1][1];
+    __builtin_amdgcn_global_load_lds(VP_GLB_PTR(base + o0), VP_LDS_PTR(dst), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(VP_GLB_PTR(base + o1), VP_LDS_PTR(dst + 1024), 16, 0, 0);
   };
 
   f32x4 acc[4][8];
@@ -105,62 +141,189 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
-  stage(0, 0);
-  wait_vmcnt0();
-  __syncthreads();
-  const int arow = wm * 128 + (lane & 15);
-  const int brow = wn * 64 + (lane & 15);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-    const char* bA = smem + cur * 65536;
-    const char* bB = bA + 32768;
+  const int l16 = lane & 15, cq = lane >> 4;
+  const int arow = wm * 64 + l16;   // local row inside an A region
+  const int brow = wn * 32 + l16;   // local row inside a B region
+  bf16x8 af[8], bf[4];
+  auto read_A = [&](const char* reg) {
+    if constexpr (DIAG & 2) { asm volatile("" : "+v"(af[0]), "+v"(af[5])); return; }
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = kk * 4 + (lane >> 4);
-      bf16x8 af[8], wf[4];
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) af[mt] = lds_frag(bA, arow + mt * 16, c);
+      for (int mt = 0; mt < 4; ++mt) af[kk * 4 + mt] = lds_frag(reg, arow + mt * 16, kk * 4 + cq);
+  };
+  auto read_B = [&](const char* reg) {
+    if constexpr (DIAG & 2) { asm volatile("" : "+v"(bf[0]), "+v"(bf[3])); return; }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) wf[nt] = lds_frag(bB, brow + nt * 16, c);
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < 2; ++nt) bf[kk * 2 + nt] = lds_frag(reg, brow + nt * 16, kk * 4 + cq);
+  };
+  auto mma = [&](int qm, int qn) {
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
-          acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt], af[mt], acc[nt][mt], 0, 0, 0);
-    }
-    wait_vmcnt0();
-    __syncthreads();
-  }
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          acc[qn * 2 + nt][qm * 4 + mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              bf[kk * 2 + nt], af[kk * 4 + mt], acc[qn * 2 + nt][qm * 4 + mt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto barrier = [] {
+    sched_fence();
+    if constexpr (!(DIAG & 4)) __builtin_amdgcn_s_barrier();
+    sched_fence();
+  };
 
-  // epilogue: lane holds D[n = nb + 4*(lane>>4) + r][m = mb + (lane&15)], r = 0..3
-  const int mb = m0 + wm * 128 + (lane & 15);
-  const int nb = n0 + wn * 64 + (lane >> 4) * 4;
-#pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    const int n = nb + nt * 16;
-    const float4 b = *reinterpret_cast<const float4*>(ep.bias + n);
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const f32x4 a = acc[nt][mt];
-      epilogue_store<EPI>(ep, N, mb + mt * 16, n, a[0] + b.x, a[1] + b.y, a[2] + b.z, a[3] + b.w);
-    }
+  // Region schedule (global K-tile g in buffer g&1; phases P1..P4 read A0+B0, B1, A1, B0):
+  //   P1(g): glds A1(g+1)   P2(g): glds B0(g+1)   P3(g): glds A0(g+2)   P4(g): glds B1(g+2)
+  // Every region is restaged >= 2 phases after its last ds_read (so reads need not be
+  // retired before the barrier), and P4's counted vmcnt(4) leaves only the two newest
+  // half-tiles in flight: all of K-tile g+1 has landed before the barrier into P1(g+1).
+  stage(RA0, 0); stage(RB0, 0); stage(RB1, 0); stage(RA1, 0);
+  if (total > 1) {
+    stage(RA0, 1); stage(RB1, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  barrier();
+  if (wm == 1) barrier();  // stagger: waves 4-7 run one barrier behind
+
+  int kt = 0, j = 0;
+  for (int g = 0; g < total; ++g) {
+    const char* cur = smem + (g & 1) * kBuf;
+    const bool s1 = g + 1 < total, s2 = g + 2 < total;
+    // P1: quadrant (0,0)
+    read_A(cur + RA0 * kRegion);
+    read_B(cur + RB0 * kRegion);
+    if (s1) stage(RA1, g + 1);
+    barrier();
+    lgkm0();
+    mma(0, 0);
+    barrier();
+    // P2: quadrant (0,1)
+    read_B(cur + RB1 * kRegion);
+    if (s1) stage(RB0, g + 1);
+    barrier();
+    lgkm0();
+    mma(0, 1);
+    barrier();
+    // P3: quadrant (1,1)
+    read_A(cur + RA1 * kRegion);
+    if (s2) stage(RA0, g + 2);
+    barrier();
+    lgkm0();
+    mma(1, 1);
+    barrier();
+    // P4: quadrant (1,0)
+    read_B(cur + RB0 * kRegion);
+    if (s2) {
+      stage(RB1, g + 2);
+      if constexpr (!(DIAG & 8)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      if constexpr (!(DIAG & 8)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    lgkm0();
+    mma(1, 0);
+    barrier();
+    if (++kt < nk) continue;
+    kt = 0;
+
+    // ---- epilogue of tile j: lane holds D[n = nb + 16*ng + 4*(lane>>4) + r][m = mb + 16*mg] ----
+    const int tile = first + j * stride;
+    ++j;
+    const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
+    const int mb = m0 + wm * 128 + l16;
+    const int nbase = n0 + wn * 64 + cq * 4;
+    float keep[8];
+#pragma unroll
+    for (int mg = 0; mg < 8; ++mg) keep[mg] = 1.0f;
+    if constexpr (EPI == EPI_GELU_BF16 || EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
+      if (ep.rowpad) {
+#pragma unroll
+        for (int mg = 0; mg < 8; ++mg) keep[mg] = 1.0f - ep.rowpad[mb + mg * 16];
+      }
+    }
+#pragma unroll
+    for (int ng = 0; ng < 4; ++ng) {
+      const int n = nbase + ng * 16;
+      const float4 bb = *reinterpret_cast<const float4*>(ep.bias + n);
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+#pragma unroll
+        for (int mg = 0; mg < 8; ++mg) {
+          const f32x4 a = acc[ng][mg];
+          float v0 = a[0] + bb.x, v1 = a[1] + bb.y, v2 = a[2] + bb.z, v3 = a[3] + bb.w;
+          if constexpr (EPI == EPI_GELU_BF16) {
+            v0 = gelu_fast(v0) * keep[mg]; v1 = gelu_fast(v1) * keep[mg];
+            v2 = gelu_fast(v2) * keep[mg]; v3 = gelu_fast(v3) * keep[mg];
+          }
+          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(ep.out) + (int64_t)(mb + mg * 16) * ep.ldo + n) =
+              make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        }
+      } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
+        float4 r[8];
+#pragma unroll
+        for (int mg = 0; mg < 8; ++mg)
+          r[mg] = *reinterpret_cast<const float4*>(ep.resid + (int64_t)(mb + mg * 16) * ep.ldr + n);
+#pragma unroll
+        for (int mg = 0; mg < 8; ++mg) {
+          const f32x4 a = acc[ng][mg];
+          const float k = keep[mg];
+          *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)(mb + mg * 16) * ep.ldo + n) =
+              make_float4(r[mg].x + (a[0] + bb.x) * k, r[mg].y + (a[1] + bb.y) * k,
+                          r[mg].z + (a[2] + bb.z) * k, r[mg].w + (a[3] + bb.w) * k);
+        }
+      } else {  // EPI_POS_F32
+        float4 p[8];
+#pragma unroll
+        for (int mg = 0; mg < 8; ++mg)
+          p[mg] = *reinterpret_cast<const float4*>(ep.pos + (int64_t)((mb + mg * 16) % ep.pos_rows) * N + n);
+#pragma unroll
+        for (int mg = 0; mg < 8; ++mg) {
+          const f32x4 a = acc[ng][mg];
+          *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)(mb + mg * 16) * ep.ldo + n) =
+              make_float4(a[0] + bb.x + p[mg].x, a[1] + bb.y + p[mg].y, a[2] + bb.z + p[mg].z,
+                          a[3] + bb.w + p[mg].w);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) acc[i][jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (wm == 0) barrier();  // balance the stagger barrier
 }
 
-template <int EPI>
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int EPI, int DIAG = 0>
 hipError_t launch_one(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                       int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<EPI, DIAG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int grid = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(gemm_bf16_tn_kernel<EPI>, dim3(grid), dim3(kGemmThreads), kGemmLds, s, A, lda,
+  const int tiles = (M / BM) * (N / BN);
+  const int grid = tiles < num_cus() ? tiles : num_cus();
+  hipLaunchKernelGGL((gemm_bf16_tn_kernel<EPI, DIAG>), dim3(grid), dim3(kGemmThreads), kGemmLds, s, A, lda,
                      W, ldw, M, N, K, ep);
   return hipGetLastError();
 }
@@ -174,6 +337,21 @@ const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw) {
   if (K % BK) return "gemm: K must be a multiple of 64";
   if (lda < K || ldw < K || (lda % 8) || (ldw % 8)) return "gemm: bad leading dimension";
   return nullptr;
+}
+
+hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
+                          int M, int N, int K, const EpiArgs& ep, hipStream_t s) {
+  switch (diag) {
+    case 0: return launch_one<EPI_BF16, 0>(A, lda, W, ldw, M, N, K, ep, s);
+    case 1: return launch_one<EPI_BF16, 1>(A, lda, W, ldw, M, N, K, ep, s);
+    case 2: return launch_one<EPI_BF16, 2>(A, lda, W, ldw, M, N, K, ep, s);
+    case 3: return launch_one<EPI_BF16, 3>(A, lda, W, ldw, M, N, K, ep, s);
+    case 4: return launch_one<EPI_BF16, 4>(A, lda, W, ldw, M, N, K, ep, s);
+    case 7: return launch_one<EPI_BF16, 7>(A, lda, W, ldw, M, N, K, ep, s);
+    case 8: return launch_one<EPI_BF16, 8>(A, lda, W, ldw, M, N, K, ep, s);
+    case 10: return launch_one<EPI_BF16, 10>(A, lda, W, ldw, M, N, K, ep, s);
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,

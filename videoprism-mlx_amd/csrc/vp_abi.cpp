@@ -647,6 +647,32 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
   return VP_OK;
 }
 
+// Not in the public header: ablation builds of the bf16 GEMM (tools/gemm_bench.py).
+int vp_dev_gemm_diag(int diag, const void* A, const void* W, int64_t M, int64_t N, int64_t K,
+                     void* out, const float* bias, void* stream) {
+  using namespace vp;
+  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  if (e) return fail(VP_EINVAL, e);
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias;
+  VP_HIP(gemm_bf16_diag(diag, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
+                        static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
+// Not in the public header: the 4-wave bf16 GEMM with any epilogue (tools/gemm_bench.py).
+int vp_dev_gemm_w4(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K,
+                   void* out, const float* bias, const float* resid, void* stream) {
+  using namespace vp;
+  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  if (e) return fail(VP_EINVAL, e);
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
+  VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
+                      static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
                     int64_t heads, float cap, const float* key_pad, void* stream) {
   using namespace vp;

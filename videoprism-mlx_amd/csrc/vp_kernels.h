@@ -32,6 +32,14 @@ const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw);
 hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                      int N, int K, const EpiArgs& ep, hipStream_t s);
 
+// 4-wave (one wave per SIMD, 128x128 per wave, 32x32x16 MFMA) decomposition
+hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                        int N, int K, const EpiArgs& ep, hipStream_t s);
+
+// ablation builds of the bf16 GEMM (store epilogue) for tools/gemm_bench.py
+hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
+                          int M, int N, int K, const EpiArgs& ep, hipStream_t s);
+
 // ---- fp32 GEMM for fprop_dtype=float32 (gemm_f32.hip) ----
 const char* gemm_f32_check(int M, int N, int K);
 hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_t ldw, int M,
