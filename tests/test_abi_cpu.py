@@ -1,0 +1,72 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/videoprism_hip.h
+declares (no compute calls here)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+from videoprism import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "videoprism_hip.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vp_\w+)\s*\(", text)))
+
+
+def test_library_present_and_loads():
+    assert os.path.exists(_native.library_path()), "build with __graft_entry__.build()"
+    lib = _native.load()
+    assert lib.vp_abi_version() == 1
+
+
+def test_every_header_symbol_exported():
+    syms = header_symbols()
+    assert len(syms) >= 18
+    lib = ctypes.CDLL(_native.library_path())
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_ctypes_bindings_cover_header():
+    assert set(header_symbols()) <= set(_native.exported_symbols())
+
+
+def test_header_compiles_as_c():
+    import subprocess
+    import tempfile
+    src = '#include "videoprism_hip.h"\nint main(void){ vp_config c; (void)c; return VP_OK; }\n'
+    with tempfile.TemporaryDirectory() as d:
+        f = os.path.join(d, "t.c")
+        open(f, "w").write(src)
+        r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HEADER),
+                            "-c", f, "-o", os.path.join(d, "t.o")], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_create_rejects_bad_configs_without_touching_a_gpu():
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    bad = _native.vp_config(patch_size=18, pos_emb_t=16, pos_emb_h=16, pos_emb_w=16, model_dim=768,
+                            num_spatial_layers=12, num_temporal_layers=4, num_heads=16, mlp_dim=3072,
+                            atten_logit_cap=50.0, fprop_dtype=1)   # dim_per_head 48
+    rc = lib.vp_create(ctypes.byref(bad), 0, ctypes.byref(h))
+    assert rc == _native.VP_ENOTSUP
+    assert b"dim_per_head" in lib.vp_last_error()
+    with pytest.raises(NotImplementedError):
+        _native.check(rc)
+    bad.num_heads = 0
+    assert lib.vp_create(ctypes.byref(bad), 0, ctypes.byref(h)) == _native.VP_EINVAL
+
+
+def test_null_arguments_are_einval():
+    lib = _native.load()
+    assert lib.vp_create(None, 0, None) == _native.VP_EINVAL
+    assert lib.vp_finalize(None) == _native.VP_EINVAL
+    assert lib.vp_forward(None, None, 0, 1, 1, 18, 18, None, None, 0, None, None, 0, None) == _native.VP_EINVAL
+    assert lib.vp_op_attention(_native.VP_BF16, None, None, 1, 256, 12, 50.0, None, None) == _native.VP_EINVAL
