@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VP_ABI_VERSION 1
+#define VP_ABI_VERSION 2
 
 typedef struct vp_handle vp_handle;
 
@@ -113,12 +113,14 @@ int vp_profile_class_name(int cls, const char** name);
 /* ---------------- op-level entry points (kernel parity tests, benches) ---------------- */
 
 /* C[M,N] = A[M,K].W[N,K]^T + bias with epilogue:
- *   0 store (out dtype = precision), 1 GELU(erf) [* (1-rowpad)], 2 out_f32 = resid + (.)*(1-rowpad),
- *   3 out_f32 = (.) + pos[m % pos_rows], 4 = 2 (separate kernel symbol used for ffn_layer2).   precision VP_BF16: A,W bf16; VP_F32: A,W fp32.
+ *   0 store (out dtype = precision), 1 GELU(erf) [* (1-rowpad)], 2 out_f32 = resid_f32 + (.)*(1-rowpad),
+ *   3 out_f32 = (.) + pos[m % pos_rows], 4 = 2 (separate kernel symbol used for ffn_layer2),
+ *   5 / 6 / 7 = 2 / 3 / 4 with a bf16 residual stream (bf16 resid and out; precision VP_BF16 only).
+ *   precision VP_BF16: A,W bf16; VP_F32: A,W fp32.
  * Replaces layers.py:273-313 (Dense) and :433-499 (einsum projections). */
 int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const void* W, int64_t ldw,
                int64_t M, int64_t N, int64_t K, void* out, int64_t ldo, const float* bias,
-               const float* resid, int64_t ldr, const float* pos, int64_t pos_rows,
+               const void* resid, int64_t ldr, const float* pos, int64_t pos_rows,
                const float* rowpad, void* stream);
 
 /* Capped attention over rows qkv[num_seq*S, 3*heads*64] = [q|k|v] (q pre-scaled), writing
@@ -127,11 +129,11 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
                     int64_t heads, float cap, const float* key_pad, void* stream);
 
-/* LayerNorm (layers.py:208-270) of fp32 rows with gamma = 1 + scale; optional row permutation
- * (0 none, 1 (b t n)->(b n t), 2 (b n t)->(b t n)) and fp32 add[t][D] by output t. */
-int vp_op_layernorm(const float* x, int64_t rows, int64_t D, const float* gamma, const float* beta,
-                    void* out, int out_dtype, int perm, int64_t T, int64_t Nsp, const float* add,
-                    void* stream);
+/* LayerNorm (layers.py:208-270) of fp32 or bf16 rows (in_dtype) with gamma = 1 + scale; optional
+ * row permutation (0 none, 1 (b t n)->(b n t), 2 (b n t)->(b t n)) and fp32 add[t][D] by output t. */
+int vp_op_layernorm(const void* x, int in_dtype, int64_t rows, int64_t D, const float* gamma,
+                    const float* beta, void* out, int out_dtype, int perm, int64_t T, int64_t Nsp,
+                    const float* add, void* stream);
 
 /* _image_to_patch (encoders.py:70-104): video [BT,H,W,C] -> patches [BT*(H/P)*(W/P), kpad]
  * with features in (p, q, c) order and zero padding from P*P*C to kpad. */

@@ -144,3 +144,24 @@ def test_full_base_b1_f32_vs_oracle(cuda):
     err = np.abs(emb - ref)
     print(f"full base f32 vs oracle-f32 max-abs {err.max():.3e} mean-abs {err.mean():.3e}")
     assert err.max() <= 2e-4
+
+
+def test_full_base_b1_bf16_vs_oracle(cuda):
+    """Full-depth videoprism_public_v1_base in bf16 (bf16 residual stream, as Flax with
+    fprop_dtype=bfloat16): the north_star bound is on the L2-normalised mean-pooled clip
+    embedding, max-abs <= 1e-3 vs the fp64 oracle; token errors are printed against both the
+    fp64 oracle and the oracle's bf16 emulation of the reference."""
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    var = params.synthetic_params(cfg, seed=0)
+    video = _video(1, 8, 288, 9, "normal")
+    mdl = models.get_model("videoprism_public_v1_base", fprop_dtype=torch.bfloat16)
+    emb, _ = mdl.apply(var, video, train=False)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    emu, _ = orc.factorized_encoder(var["params"], video, cfg, mode="bf16")
+    err, err_emu = np.abs(emb - ref), np.abs(emb - emu)
+    perr = np.abs(_pool_l2(emb) - _pool_l2(ref))
+    print(f"full base bf16: vs f64 token mean-abs {err.mean():.3e} max {err.max():.3e}; vs bf16-emulation "
+          f"mean-abs {err_emu.mean():.3e}; reference-emulation vs f64 mean-abs {np.abs(emu - ref).mean():.3e}; "
+          f"pooled-l2 max-abs {perr.max():.3e}")
+    assert perr.max() <= 1e-3
+    assert err.mean() <= 3e-2

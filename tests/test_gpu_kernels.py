@@ -81,6 +81,89 @@ def test_gemm_bf16_pos(cuda):
     assert float((out.double() - ref).abs().max()) < 1e-4
 
 
+@pytest.mark.parametrize("epi", [nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16])
+def test_gemm_bf16_resid_bf16_stream(cuda, epi):
+    """bf16 residual stream (fprop_dtype bf16 keeps x in bf16, models.py:301-302): out =
+    bf16(x + (a.w^T + b) * keep), one rounding -> |err| <= 2^-8 |ref| + fp32-accumulation slack."""
+    M, N, K = 2048, 768, 3072 if epi == nat.EPI_RESID_FFN_BF16 else 768
+    g = torch.Generator(device="cpu").manual_seed(21 + epi)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    x = _bf(torch.randn(M, N, generator=g) * 4).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.25).float().to(cuda)
+    ref = x.double() + (a.double() @ w.double().T + b.double()) * (1 - pad.double())[:, None]
+    nat.op_gemm(a, w, b, epi, out=x, resid=x, rowpad=pad)
+    torch.cuda.synchronize()
+    assert x.dtype == torch.bfloat16
+    err = (x.double() - ref).abs()
+    assert bool((err <= 2 ** -8 * ref.abs() + 1e-4).all()), float(err.max())
+
+
+def test_gemm_bf16_pos_bf16(cuda):
+    M, N, K = 1024, 768, 1024
+    g = torch.Generator(device="cpu").manual_seed(6)
+    a = _bf(torch.rand(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pos = torch.randn(256, N, generator=g).to(cuda)
+    out = nat.op_gemm(a, w, b, nat.EPI_POS_BF16, pos=pos)
+    torch.cuda.synchronize()
+    assert out.dtype == torch.bfloat16
+    ref = a.double() @ w.double().T + b.double() + pos.double().repeat(M // 256, 1)
+    err = (out.double() - ref).abs()
+    assert bool((err <= 2 ** -8 * ref.abs() + 1e-4).all()), float(err.max())
+
+
+# both bf16 GEMM kernels on persistent shapes: tiles > CUs (several tiles per workgroup, so the
+# K-tile stream crosses tile boundaries), tile counts not divisible by 8 XCDs, K = 1..48 K-tiles
+KERNEL_SHAPES = [(16384, 2304, 768), (32768, 768, 3072), (2304, 1536, 64), (512, 256, 1024)]
+
+
+@pytest.mark.parametrize("M,N,K", KERNEL_SHAPES)
+@pytest.mark.parametrize("epi", [nat.EPI_STORE, nat.EPI_GELU, nat.EPI_RESID, nat.EPI_POS,
+                                 nat.EPI_RESID_FFN, nat.EPI_RESID_BF16, nat.EPI_POS_BF16,
+                                 nat.EPI_RESID_FFN_BF16])
+def test_gemm_kernels_bitwise_equal(cuda, M, N, K, epi):
+    """The 4-wave and 8-wave kernels sum each output's K products in the same order (k-halves of
+    32 in sequence, fp32 MFMA accumulation), so they must agree bit for bit on every epilogue;
+    one of them is additionally checked against fp64."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.2).float().to(cuda)
+    pos = torch.randn(256, N, generator=g).to(cuda) if epi in (nat.EPI_POS, nat.EPI_POS_BF16) else None
+    f32_out = epi in (nat.EPI_RESID, nat.EPI_POS, nat.EPI_RESID_FFN)
+    resid = epi in (nat.EPI_RESID, nat.EPI_RESID_FFN, nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16)
+    x0 = torch.randn(M, N, generator=g).to(cuda)
+    outs = {}
+    for which in (4, 8):
+        if resid:
+            o = x0.clone() if f32_out else x0.to(torch.bfloat16)
+        else:
+            o = torch.empty(M, N, device=cuda, dtype=torch.float32 if f32_out else torch.bfloat16)
+        nat.dev_gemm_kernel(which, a, w, b, epi, o, resid=o if resid else None, pos=pos,
+                            rowpad=pad if epi != nat.EPI_POS and epi != nat.EPI_POS_BF16 else None)
+        outs[which] = o
+    torch.cuda.synchronize()
+    assert torch.equal(outs[4], outs[8])
+    y = a.double() @ w.double().T + b.double()
+    keep = (1 - pad.double())[:, None]
+    if epi == nat.EPI_STORE:
+        ref = y
+    elif epi == nat.EPI_GELU:
+        ref = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) * keep
+    elif epi in (nat.EPI_POS, nat.EPI_POS_BF16):
+        ref = y + pos.double().repeat(M // 256, 1)
+    else:
+        xr = x0.double() if f32_out else x0.to(torch.bfloat16).double()
+        ref = xr + y * keep
+    err = (outs[4].double() - ref).abs()
+    tol = (1e-4 if f32_out else 2 ** -8 * ref.abs() + 1e-4) + 5e-6 * K ** 0.5
+    assert bool((err <= tol).all()), float(err.max())
+
+
 def test_gemm_bf16_asymmetric_identity(cuda):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     M = N = K = 256
@@ -192,10 +275,13 @@ def test_attention_f32(cuda, S, num_seq, heads):
 @pytest.mark.parametrize("D,perm", [(768, nat.PERM_NONE), (768, nat.PERM_BTN_TO_BNT),
                                     (1024, nat.PERM_BNT_TO_BTN)])
 @pytest.mark.parametrize("out_bf16", [False, True])
-def test_layernorm(cuda, D, perm, out_bf16):
+@pytest.mark.parametrize("in_bf16", [False, True])
+def test_layernorm(cuda, D, perm, out_bf16, in_bf16):
     B, T, N = 2, 4, 256
     g = torch.Generator(device="cpu").manual_seed(D + perm)
     x = (torch.randn(B * T * N, D, generator=g) * 3 + 1).to(cuda)
+    if in_bf16:  # bf16 residual stream: the reference value is the LN of the bf16 input
+        x = x.to(torch.bfloat16)
     scale = torch.randn(D, generator=g) * 0.1
     bias = torch.randn(D, generator=g) * 0.1
     add = torch.randn(T, D, generator=g).to(cuda) if perm == nat.PERM_BTN_TO_BNT else None

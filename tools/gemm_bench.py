@@ -1,8 +1,14 @@
-"""GEMM microbenchmark at the encoder's shapes: our HIP kernel (vp_op_gemm) vs
-torch.matmul (hipBLASLt) as a known-good reference on the same device and data."""
+"""GEMM microbenchmark at the encoder's shapes: both HIP kernels (4-wave `gemm_bf16_w4`,
+8-wave `gemm_bf16`) with the forward's epilogues, against torch.matmul (hipBLASLt) as a
+known-good reference on the same device and data (no epilogue on the torch side).
+
+  python tools/gemm_bench.py            # kernels vs torch, plus w4 == w8 bitwise check
+  python tools/gemm_bench.py w4var      # 4-wave ablation builds (DIAG bits, see the kernel)
+  python tools/gemm_bench.py w8var      # 8-wave ablation builds
+"""
+import ctypes
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
@@ -10,11 +16,12 @@ import torch  # noqa: E402
 
 from videoprism import _native as nat  # noqa: E402
 
-SHAPES = [  # name, M, N, K, epilogue
-    ("qkv", 131072, 2304, 768, nat.EPI_STORE),
-    ("post", 131072, 768, 768, nat.EPI_RESID),
-    ("ffn1", 131072, 3072, 768, nat.EPI_GELU),
-    ("ffn2", 131072, 768, 3072, nat.EPI_RESID_FFN),
+M_TOK = 131072  # B=32 clips x 16 frames x 256 patches
+SHAPES = [  # name, M, N, K, epilogue (as in vp_forward's bf16 path)
+    ("qkv", M_TOK, 2304, 768, nat.EPI_STORE),
+    ("post", M_TOK, 768, 768, nat.EPI_RESID_BF16),
+    ("ffn1", M_TOK, 3072, 768, nat.EPI_GELU),
+    ("ffn2", M_TOK, 768, 3072, nat.EPI_RESID_FFN_BF16),
 ]
 
 
@@ -31,68 +38,74 @@ def timeit(fn, iters=20, warm=3):
     return s.elapsed_time(e) / iters
 
 
-def variants(dev, g):
-    import ctypes
-    lib = nat.load()
-    fn = lib.vp_dev_gemm_diag
-    fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
-                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-    for name, M, N, K, _ in SHAPES:
-        a = (torch.rand((M, K), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
-        w = ((torch.rand((N, K), generator=g, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
-        b = torch.zeros(N, device=dev)
-        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        s = torch.cuda.current_stream().cuda_stream
-        res = {v: [] for v in (0, 1, 8, 2, 10, 3)}
-        for rnd in range(3):  # interleaved rounds (rule 24)
-            for v in res:
-                f = lambda: nat.check(fn(v, a.data_ptr(), w.data_ptr(), M, N, K, o.data_ptr(), b.data_ptr(), s))
-                res[v].append(timeit(f, iters=10, warm=2))
+def operands(M, N, K, g, dev):
+    a = (torch.rand((M, K), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand((N, K), generator=g, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+    b = torch.zeros(N, device=dev)
+    return a, w, b
+
+
+def compare(dev, g):
+    for name, M, N, K, epi in SHAPES:
+        a, w, b = operands(M, N, K, g, dev)
+        resid = epi in (nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16)
+        x0 = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16) if resid else None
+        outs = {}
+        for which in (8, 4):
+            o = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+            nat.dev_gemm_kernel(which, a, w, b, epi, o, resid=o if resid else None)
+            outs[which] = o
+        torch.cuda.synchronize()
+        same = bool(torch.equal(outs[4], outs[8]))
+        del outs
+        o = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        f8 = lambda: nat.dev_gemm_kernel(8, a, w, b, epi, o, resid=o if resid else None)
+        f4 = lambda: nat.dev_gemm_kernel(4, a, w, b, epi, o, resid=o if resid else None)
+        res = {"w8": [], "w4": [], "torch": []}
+        for _ in range(3):  # interleaved rounds
+            res["w8"].append(timeit(f8))
+            res["w4"].append(timeit(f4))
+            res["torch"].append(timeit(lambda: torch.matmul(a, w.t())))
         flop = 2.0 * M * N * K
-        print(name, "diag", " ".join(f"d{v}:{flop/min(t)/1e9:6.1f}TF" for v, t in res.items()), flush=True)
+        print(f"{name:5s} M={M} N={N} K={K} epi={epi} w4==w8:{same}: " + " | ".join(
+            f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
+
+
+def variants(dev, g, which, diags):
+    for name, M, N, K, _ in SHAPES:
+        a, w, b = operands(M, N, K, g, dev)
+        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        st = torch.cuda.current_stream().cuda_stream
+        res = {d: [] for d in diags}
+        for _ in range(3):
+            for d in diags:
+                if which == 4:
+                    f = lambda: nat.dev_gemm_kernel(4, a, w, b, (1000 + d) if d else 0, o)
+                else:
+                    lib = nat.load()
+                    fn = lib.vp_dev_gemm_diag
+                    fn.restype = ctypes.c_int
+                    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+                    f = lambda: nat.check(fn(d, a.data_ptr(), w.data_ptr(), M, N, K, o.data_ptr(),
+                                             b.data_ptr(), st))
+                res[d].append(timeit(f, iters=10, warm=2))
+        flop = 2.0 * M * N * K
+        print(f"{name} w{which} ablations:", " ".join(f"d{d}:{flop/min(t)/1e9:6.1f}TF" for d, t in res.items()),
+              "| us:", " ".join(f"d{d}:{min(t)*1e3:6.1f}" for d, t in res.items()), flush=True)
 
 
 def main():
-    only = sys.argv[1:]
-    if only == ["variants"]:
-        variants(torch.device("cuda:0"), torch.Generator(device="cuda:0").manual_seed(0))
-        return
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    for name, M, N, K, epi in SHAPES:
-        if only and name not in only:
-            continue
-        a = (torch.rand((M, K), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
-        w = ((torch.rand((N, K), generator=g, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
-        b = torch.zeros(N, device=dev)
-        x = torch.zeros((M, N), device=dev)
-        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        flop = 2.0 * M * N * K
-        if epi in (nat.EPI_RESID, nat.EPI_RESID_FFN):
-            f = lambda: nat.op_gemm(a, w, b, epi, out=x, resid=x)
-        else:
-            f = lambda: nat.op_gemm(a, w, b, epi, out=o)
-        import ctypes
-        lib = nat.load()
-        w4 = lib.vp_dev_gemm_w4
-        w4.restype = ctypes.c_int
-        w4.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
-                       ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-        st = torch.cuda.current_stream().cuda_stream
-        outp = x if epi in (nat.EPI_RESID, nat.EPI_RESID_FFN) else o
-        g4 = lambda: nat.check(w4(epi, a.data_ptr(), w.data_ptr(), M, N, K, outp.data_ptr(), b.data_ptr(), x.data_ptr(), st))
-        if epi in (nat.EPI_STORE, nat.EPI_GELU):
-            ref_o = nat.op_gemm(a, w, b, epi, out=torch.empty_like(o)).float()
-            g4(); torch.cuda.synchronize()
-            print(f"  w4 vs w8 max|diff| {float((o.float() - ref_o).abs().max()):.3e}")
-        res = {"w8": [], "w4": [], "torch": []}
-        for _ in range(3):
-            res["w8"].append(timeit(f))
-            res["w4"].append(timeit(g4))
-            res["torch"].append(timeit(lambda: torch.matmul(a, w.t())))
-        print(f"{name:5s} M={M} N={N} K={K}: " + " | ".join(
-            f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
+    mode = sys.argv[1] if len(sys.argv) > 1 else ""
+    if mode == "w4var":
+        variants(dev, g, 4, [0, 2, 4, 6])
+    elif mode == "w8var":
+        variants(dev, g, 8, [0, 1, 2, 8, 16])
+    else:
+        compare(dev, g)
 
 
 if __name__ == "__main__":

@@ -50,10 +50,10 @@ __global__ __launch_bounds__(256) void patchify_kernel(const TI* __restrict__ vi
   }
 }
 
-// ---- LayerNorm (layers.py:208-270) over fp32 rows, one wave per row ----
-// NCH = D / 256 float4 chunks per lane.  gamma = 1 + scale (folded on the host).
-template <int NCH, bool OUT_BF16>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int rows,
+// ---- LayerNorm (layers.py:208-270) over fp32 or bf16 rows, one wave per row ----
+// NCH = D / 256 4-element chunks per lane.  gamma = 1 + scale (folded on the host).
+template <int NCH, bool OUT_BF16, bool IN_BF16>
+__global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x, int rows,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         void* __restrict__ out, int perm, int T,
@@ -62,12 +62,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* xr = x + (int64_t)row * D;
   float4 v[NCH];
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    v[c] = *reinterpret_cast<const float4*>(xr + c * 256 + lane * 4);
+    if constexpr (IN_BF16) {
+      const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(x) + (int64_t)row * D +
+                                                      c * 256 + lane * 4);
+      v[c] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                         __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    } else {
+      v[c] = *reinterpret_cast<const float4*>(static_cast<const float*>(x) + (int64_t)row * D + c * 256 +
+                                              lane * 4);
+    }
     s += (v[c].x + v[c].y) + (v[c].z + v[c].w);
   }
 #pragma unroll
@@ -179,15 +186,24 @@ int grid_for(int64_t work, int block) {
 }
 
 template <int NCH>
-hipError_t ln_launch(const float* x, int rows, const float* gamma, const float* beta, void* out,
-                     int out_is_bf16, int perm, int T, int Nsp, const float* add, hipStream_t s) {
+hipError_t ln_launch(const void* x, int in_is_bf16, int rows, const float* gamma, const float* beta,
+                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add, hipStream_t s) {
   const dim3 grid((rows + 3) / 4);
-  if (out_is_bf16)
-    hipLaunchKernelGGL((layernorm_kernel<NCH, true>), grid, dim3(256), 0, s, x, rows, gamma, beta,
-                       out, perm, T, Nsp, add);
-  else
-    hipLaunchKernelGGL((layernorm_kernel<NCH, false>), grid, dim3(256), 0, s, x, rows, gamma, beta,
-                       out, perm, T, Nsp, add);
+  if (in_is_bf16) {
+    if (out_is_bf16)
+      hipLaunchKernelGGL((layernorm_kernel<NCH, true, true>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+                         out, perm, T, Nsp, add);
+    else
+      hipLaunchKernelGGL((layernorm_kernel<NCH, false, true>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+                         out, perm, T, Nsp, add);
+  } else {
+    if (out_is_bf16)
+      hipLaunchKernelGGL((layernorm_kernel<NCH, true, false>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+                         out, perm, T, Nsp, add);
+    else
+      hipLaunchKernelGGL((layernorm_kernel<NCH, false, false>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+                         out, perm, T, Nsp, add);
+  }
   return hipGetLastError();
 }
 
@@ -216,17 +232,17 @@ hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is
   return hipGetLastError();
 }
 
-hipError_t layernorm(const float* x, int rows, int D, const float* gamma, const float* beta,
-                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add,
-                     hipStream_t s) {
+hipError_t layernorm(const void* x, int in_is_bf16, int rows, int D, const float* gamma,
+                     const float* beta, void* out, int out_is_bf16, int perm, int T, int Nsp,
+                     const float* add, hipStream_t s) {
   switch (D) {
-    case 256: return ln_launch<1>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 512: return ln_launch<2>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 768: return ln_launch<3>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 1024: return ln_launch<4>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 1280: return ln_launch<5>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 1536: return ln_launch<6>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 2048: return ln_launch<8>(x, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 256: return ln_launch<1>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 512: return ln_launch<2>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 768: return ln_launch<3>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 1024: return ln_launch<4>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 1280: return ln_launch<5>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 1536: return ln_launch<6>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 2048: return ln_launch<8>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
   }
   return hipErrorInvalidValue;
 }

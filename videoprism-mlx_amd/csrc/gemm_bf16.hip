@@ -27,8 +27,10 @@
 //  * Persistent grid (one workgroup per CU) with a K-tile stream that runs across tiles,
 //    so the next tile's loads overlap this tile's epilogue; each XCD owns a contiguous
 //    tile chunk (L2 locality for A panels and W).
-#include "vp_common.h"
-#include "vp_kernels.h"
+#include "gemm_epilogue.h"
+
+#include <cstdlib>
+#include <cstring>
 
 namespace vp {
 
@@ -47,19 +49,6 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* region, int row, int chun
   return *reinterpret_cast<const bf16x8*>(region + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
-// A&S 7.1.26 erf (|err| <= 1.5e-7) folded into GELU: 0.5*(x + |x|*erf(|x|/sqrt2)).
-__device__ __forceinline__ float gelu_fast(float x) {
-  const float ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f(x * x * (-0.5f * 1.4426950408889634f));
-  const float erf_abs = fmaf(-p, e, 1.0f);
-  return 0.5f * fmaf(ax, erf_abs, x);
-}
 
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
@@ -70,7 +59,8 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // one, and its epilogue runs while they are in flight (no per-tile pipeline drain).
 // DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 1 = no glds in
 // the K loop, 2 = no ds_reads in the K loop, 4 = no barriers in the K loop, 8 = glds issued
-// but no vmcnt wait in the K loop.
+// but no vmcnt wait in the K loop, 16 = register staging (global_load_dwordx4 two phases
+// ahead, ds_write_b128 when the region is free) instead of global_load_lds.
 template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -135,6 +125,40 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     __builtin_amdgcn_global_load_lds(VP_GLB_PTR(base + o1), VP_LDS_PTR(dst + 1024), 16, 0, 0);
   };
 
+  // ---- register staging (DIAG & 16): per-lane linear source chunk, swizzled LDS write ----
+  constexpr bool kReg = DIAG & 16;
+  bf16x8 stg[2][2];
+  int64_t roffA[2][2], roffB[2][2];
+  int wdst[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rl = (w * 2 + i) * 8 + (lane >> 3);
+    wdst[i] = rl * 128 + (((lane & 7) ^ swz(rl)) << 4);
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      roffA[qq][i] = (int64_t)(((rl >> 6) << 7) + qq * 64 + (rl & 63)) * lda + (lane & 7) * 8;
+      roffB[qq][i] = (int64_t)(((rl >> 5) << 6) + qq * 32 + (rl & 31)) * ldw + (lane & 7) * 8;
+    }
+  }
+  auto gload = [&](int region, int g, int slot) {
+    g = g < total ? g : total - 1;
+    int tm, tn, kt;
+    tile_of(g, tm, tn, kt);
+    const bf16_t* base = region < 2 ? A + (int64_t)tm * BM * lda + kt * BK
+                                    : W + (int64_t)tn * BN * ldw + kt * BK;
+    const int64_t o0 = region == RA0 ? roffA[0][0] : region == RA1 ? roffA[1][0]
+                     : region == RB0 ? roffB[0][0] : roffB[1][0];
+    const int64_t o1 = region == RA0 ? roffA[0][1] : region == RA1 ? roffA[1][1]
+                     : region == RB0 ? roffB[0][1] : roffB[1][1];
+    stg[slot][0] = *reinterpret_cast<const bf16x8*>(base + o0);
+    stg[slot][1] = *reinterpret_cast<const bf16x8*>(base + o1);
+  };
+  auto swrite = [&](int region, int g, int slot) {
+    char* dst = smem + (g & 1) * kBuf + region * kRegion;
+    *reinterpret_cast<bf16x8*>(dst + wdst[0]) = stg[slot][0];
+    *reinterpret_cast<bf16x8*>(dst + wdst[1]) = stg[slot][1];
+  };
+
   f32x4 acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -183,6 +207,20 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   // Every region is restaged >= 2 phases after its last ds_read (so reads need not be
   // retired before the barrier), and P4's counted vmcnt(4) leaves only the two newest
   // half-tiles in flight: all of K-tile g+1 has landed before the barrier into P1(g+1).
+  if constexpr (kReg) {
+    // prologue: K-tile 0 and A0/B1 of K-tile 1 written directly; A1(1) -> slot 0, B0(1) -> slot 1
+    const int pro[6][2] = {{RA0, 0}, {RB0, 0}, {RB1, 0}, {RA1, 0}, {RA0, 1}, {RB1, 1}};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      gload(pro[i][0], pro[i][1], 0);
+      swrite(pro[i][0], pro[i][1] < total ? pro[i][1] : 0, 0);
+    }
+    gload(RA1, 1, 0);
+    gload(RB0, 1, 1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the prologue ds_writes
+    barrier();
+    if (wm == 1) barrier();
+  } else {
   stage(RA0, 0); stage(RB0, 0); stage(RB1, 0); stage(RA1, 0);
   if (total > 1) {
     stage(RA0, 1); stage(RB1, 1);
@@ -192,6 +230,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   }
   barrier();
   if (wm == 1) barrier();  // stagger: waves 4-7 run one barrier behind
+  }
 
   int kt = 0, j = 0;
   for (int g = 0; g < total; ++g) {
@@ -200,28 +239,45 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     // P1: quadrant (0,0)
     read_A(cur + RA0 * kRegion);
     read_B(cur + RB0 * kRegion);
-    if (s1) stage(RA1, g + 1);
+    if constexpr (kReg) {  // write A1(g+1) (loaded 2 phases ago), load A0(g+2)
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      swrite(RA1, g + 1, 0);
+      gload(RA0, g + 2, 0);
+    } else if (s1) stage(RA1, g + 1);
     barrier();
     lgkm0();
     mma(0, 0);
     barrier();
     // P2: quadrant (0,1)
     read_B(cur + RB1 * kRegion);
-    if (s1) stage(RB0, g + 1);
+    if constexpr (kReg) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      swrite(RB0, g + 1, 1);
+      gload(RB1, g + 2, 1);
+    } else if (s1) stage(RB0, g + 1);
     barrier();
     lgkm0();
     mma(0, 1);
     barrier();
     // P3: quadrant (1,1)
     read_A(cur + RA1 * kRegion);
-    if (s2) stage(RA0, g + 2);
+    if constexpr (kReg) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      swrite(RA0, g + 2, 0);
+      gload(RA1, g + 2, 0);
+    } else if (s2) stage(RA0, g + 2);
     barrier();
     lgkm0();
     mma(1, 1);
     barrier();
     // P4: quadrant (1,0)
     read_B(cur + RB0 * kRegion);
-    if (s2) {
+    if constexpr (kReg) {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      swrite(RB1, g + 2, 1);
+      gload(RB0, g + 2, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K-tile g+1 written before the barrier
+    } else if (s2) {
       stage(RB1, g + 2);
       if constexpr (!(DIAG & 8)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
@@ -240,10 +296,11 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
     const int mb = m0 + wm * 128 + l16;
     const int nbase = n0 + wn * 64 + cq * 4;
+    using Tr = EpiTraits<EPI>;
     float keep[8];
 #pragma unroll
     for (int mg = 0; mg < 8; ++mg) keep[mg] = 1.0f;
-    if constexpr (EPI == EPI_GELU_BF16 || EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
+    if constexpr (Tr::kKeep) {
       if (ep.rowpad) {
 #pragma unroll
         for (int mg = 0; mg < 8; ++mg) keep[mg] = 1.0f - ep.rowpad[mb + mg * 16];
@@ -253,43 +310,14 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     for (int ng = 0; ng < 4; ++ng) {
       const int n = nbase + ng * 16;
       const float4 bb = *reinterpret_cast<const float4*>(ep.bias + n);
-      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+      float4 ex[8];  // residual / position rows, all issued before the first store
 #pragma unroll
-        for (int mg = 0; mg < 8; ++mg) {
-          const f32x4 a = acc[ng][mg];
-          float v0 = a[0] + bb.x, v1 = a[1] + bb.y, v2 = a[2] + bb.z, v3 = a[3] + bb.w;
-          if constexpr (EPI == EPI_GELU_BF16) {
-            v0 = gelu_fast(v0) * keep[mg]; v1 = gelu_fast(v1) * keep[mg];
-            v2 = gelu_fast(v2) * keep[mg]; v3 = gelu_fast(v3) * keep[mg];
-          }
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(ep.out) + (int64_t)(mb + mg * 16) * ep.ldo + n) =
-              make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-        }
-      } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
-        float4 r[8];
+      for (int mg = 0; mg < 8; ++mg) ex[mg] = epi_extra<EPI>(ep, mb + mg * 16, n, N);
 #pragma unroll
-        for (int mg = 0; mg < 8; ++mg)
-          r[mg] = *reinterpret_cast<const float4*>(ep.resid + (int64_t)(mb + mg * 16) * ep.ldr + n);
-#pragma unroll
-        for (int mg = 0; mg < 8; ++mg) {
-          const f32x4 a = acc[ng][mg];
-          const float k = keep[mg];
-          *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)(mb + mg * 16) * ep.ldo + n) =
-              make_float4(r[mg].x + (a[0] + bb.x) * k, r[mg].y + (a[1] + bb.y) * k,
-                          r[mg].z + (a[2] + bb.z) * k, r[mg].w + (a[3] + bb.w) * k);
-        }
-      } else {  // EPI_POS_F32
-        float4 p[8];
-#pragma unroll
-        for (int mg = 0; mg < 8; ++mg)
-          p[mg] = *reinterpret_cast<const float4*>(ep.pos + (int64_t)((mb + mg * 16) % ep.pos_rows) * N + n);
-#pragma unroll
-        for (int mg = 0; mg < 8; ++mg) {
-          const f32x4 a = acc[ng][mg];
-          *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)(mb + mg * 16) * ep.ldo + n) =
-              make_float4(a[0] + bb.x + p[mg].x, a[1] + bb.y + p[mg].y, a[2] + bb.z + p[mg].z,
-                          a[3] + bb.w + p[mg].w);
-        }
+      for (int mg = 0; mg < 8; ++mg) {
+        const f32x4 a = acc[ng][mg];
+        epi_store<EPI>(ep, mb + mg * 16, n, make_float4(a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w),
+                       keep[mg], ex[mg]);
       }
     }
 #pragma unroll
@@ -350,6 +378,7 @@ hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* 
     case 7: return launch_one<EPI_BF16, 7>(A, lda, W, ldw, M, N, K, ep, s);
     case 8: return launch_one<EPI_BF16, 8>(A, lda, W, ldw, M, N, K, ep, s);
     case 10: return launch_one<EPI_BF16, 10>(A, lda, W, ldw, M, N, K, ep, s);
+    case 16: return launch_one<EPI_BF16, 16>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }
@@ -362,8 +391,30 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
     case EPI_RESID_F32: return launch_one<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_F32: return launch_one<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN: return launch_one<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16: return launch_one<EPI_RESID_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_BF16: return launch_one<EPI_POS_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16: return launch_one<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
+}
+
+// Kernel choice for the forward and vp_op_gemm.  VP_GEMM_KERNEL=w8|w4 forces one kernel
+// (A/B runs of tools/ and bench.py); default: the 4-wave kernel wherever its 32-bit buffer
+// offsets reach, except the shapes where the 8-wave kernel measured faster.
+hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                          int N, int K, const EpiArgs& ep, hipStream_t s) {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("VP_GEMM_KERNEL");
+    mode = (e && !strcmp(e, "w8")) ? 8 : (e && !strcmp(e, "w4")) ? 4 : 0;
+  }
+  const bool w4_ok = (uint64_t)M * (uint64_t)lda * 2 < 0xFFFFFFF0ull &&
+                     (uint64_t)N * (uint64_t)ldw * 2 < 0xFFFFFFF0ull;
+  bool use_w4 = w4_ok;
+  if (mode == 8) use_w4 = false;
+  else if (mode == 0 && (epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024) use_w4 = false;
+  if (use_w4) return gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s);
+  return gemm_bf16(epi, A, lda, W, ldw, M, N, K, ep, s);
 }
 
 }  // namespace vp

@@ -1,23 +1,29 @@
-// bf16 GEMM, 4-wave decomposition (one wave per SIMD, 128x128 per wave).
+// bf16 GEMM, 4-wave decomposition (one wave per SIMD, 128x128 per wave), persistent.
 //
 //   C[M,N] = A[M,K] . W[N,K]^T  (+ epilogue), 256x256 tile, BK = 64, 256 threads.
 //
-// Why this shape on MI355X (measured, tools/gemm_bench.py ablations):
-// with 8 waves of 128x64 the CU reads 224 KiB of LDS per K-tile and the LDS-DMA issue of
-// the staging loads competes with it; removing the DMA instructions alone was worth +32%.
-// 4 waves of 128x128 read 128 KiB per K-tile, and v_mfma_f32_32x32x16_bf16 (32 cycles,
-// issue held for 8) leaves 24 free issue cycles per MFMA in which each wave's 16
-// global_load_lds and 32 ds_read_b128 per K-tile are interleaved.  The 256 fp32
-// accumulators live in the AGPR half of the 512-entry register file.
-//
-// Pipeline: 2 LDS buffers (2 x 64 KiB).  K-tile t+1 is staged into the other buffer while
-// K-tile t is computed (its buffer was released by the barrier that ended t-1); fragments
-// of k-step s+1 are read while the 16 MFMAs of k-step s run; one vmcnt(0) + barrier per
-// K-tile.  Same source-side bank swizzle and epilogue conventions as gemm_bf16.hip.
-#include <type_traits>
-
-#include "vp_common.h"
-#include "vp_kernels.h"
+// Why this shape on MI355X (measured with tools/gemm_bench.py):
+//  * 8 waves of 128x64 (gemm_bf16.hip) read 2x the LDS bytes per FLOP of 4 waves of
+//    128x128 and every staging instruction competes with the partner wave's MFMAs.  Here the
+//    512-entry register file of a SIMD belongs to one wave: 256 fp32 accumulators (8x8
+//    blocks of v_mfma_f32_16x16x32_bf16) in AGPRs, two fragment sets (k-halves) in VGPRs.
+//  * Staging moves FULL 128-byte lines: a piece is 8 rows x 128 B (one K-tile of 8 rows),
+//    loaded by buffer_load_dwordx4 ... lds (SGPR descriptor, constant per-lane voffset, tile
+//    and K offsets in soffset).  Half-line (64 B) pieces measured 15-18% slower.
+//  * Two 64 KiB K-tile buffers.  K-tile g is computed as two k-halves h0/h1 of 64 MFMAs:
+//      h0: MFMAs on set 0, ds_read set 1 <- (g, h1)                      (no barrier)
+//      h1: lgkmcnt(0) vmcnt(0) barrier; MFMAs on set 1, ds_read set 0 <- (g+1, h0),
+//          16 loads of K-tile g+2 into buffer g&1 (free: its last reads retired before the
+//          barrier).  Those loads have ~1.5 halves before the next h1 barrier waits on them
+//          (a 2-half window measured as good as 3; 1 half costs 10%).
+//  * 128-byte LDS rows, swizzle chunk ^= (row >> 1) & 7 applied on the global source (the
+//    LDS-DMA image is lane-linear) and undone on the ds_read_b128 (conflict-free for the
+//    16x16x32 operand reads).
+//  * W is the MFMA A-operand, so each lane's accumulators hold 4 consecutive N columns of
+//    one M row (8-byte bf16 / 16-byte fp32 stores), as in gemm_bf16.hip.
+//  * The K-tile stream runs across the persistent workgroup's tiles: the next tile's first
+//    K-tiles load during this tile's last K-tiles and epilogue.
+#include "gemm_epilogue.h"
 
 namespace vp {
 
@@ -25,197 +31,244 @@ namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64;
 constexpr int kThreads = 256;
-constexpr int kTileBytes = BM * BK * 2;      // 32 KiB per operand per K-tile
-constexpr int kBuf = 2 * kTileBytes;         // A then W
+constexpr int kOp = BM * BK * 2;             // 32 KiB: one operand's K-tile
+constexpr int kBuf = 2 * kOp;                // A then W
 constexpr int kLds = 2 * kBuf;               // 128 KiB
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
-__device__ __forceinline__ bf16x8 frag(const char* base, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(base + row * 128 + ((chunk ^ swz(row)) << 4));
-}
 
-__device__ __forceinline__ float gelu_fast(float x) {
-  const float ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f(x * x * (-0.5f * 1.4426950408889634f));
-  return 0.5f * fmaf(ax, fmaf(-p, e, 1.0f), x);
-}
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
-template <int EPI>
+// DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 2 = no ds_reads
+// in the K loop, 4 = no staging loads after the prologue.
+template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, EpiArgs ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = N / BN;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int m0 = (wgid / tilesN) * BM, n0 = (wgid % tilesN) * BN;
+  const int T = (M / BM) * tilesN;
+  const int G = gridDim.x;
+  const int b = blockIdx.x;
+  int first, stride, count;
+  if ((G & 7) == 0) {  // XCD x owns tiles [x*T/8, (x+1)*T/8), tn fastest
+    const int xcd = b & 7, li = b >> 3, nx = G >> 3;
+    const int lo = (int)(((int64_t)xcd * T) >> 3), hi = (int)(((int64_t)(xcd + 1) * T) >> 3);
+    first = lo + li;
+    stride = nx;
+    count = first < hi ? (hi - first + nx - 1) / nx : 0;
+  } else {
+    first = b;
+    stride = G;
+    count = b < T ? (T - b + G - 1) / G : 0;
+  }
+  if (count == 0) return;
   const int lane = threadIdx.x & 63;
   const int w = wave_id();
   const int wm = w >> 1, wn = w & 1;
-
-  // staging: wave w fills pieces w*8 + i (i = 0..7) of A and of W; piece = 8 rows x 128 B.
-  // Row of piece i: w*64 + i*8 + (lane>>3); its swizzled chunk depends only on i & 1.
-  const int r0 = w * 64 + (lane >> 3);
-  const int c_even = (lane & 7) ^ swz(r0);
-  const int c_odd = (lane & 7) ^ swz(r0 + 8);
-  const bf16_t* a_even = A + (int64_t)(m0 + r0) * lda + c_even * 8;
-  const bf16_t* a_odd = A + (int64_t)(m0 + r0 + 8) * lda + c_odd * 8;
-  const bf16_t* w_even = W + (int64_t)(n0 + r0) * ldw + c_even * 8;
-  const bf16_t* w_odd = W + (int64_t)(n0 + r0 + 8) * ldw + c_odd * 8;
-  const int64_t a16 = 16 * lda, w16 = 16 * ldw;
-  // piece p (0..15) of this wave for one K-tile: p < 8 -> A piece p, else W piece p-8
-  auto stage_piece = [&](int buf, int kt, int p) {
-    const int i = p & 7;
-    const bool isW = p >= 8;
-    const bf16_t* src = isW ? ((i & 1) ? w_odd : w_even) + (i >> 1) * w16
-                            : ((i & 1) ? a_odd : a_even) + (i >> 1) * a16;
-    char* dst = smem + buf * kBuf + (isW ? kTileBytes : 0) + (w * 8 + i) * 1024;
-    __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src + kt * BK), VP_LDS_PTR(dst), 16, 0, 0);
-  };
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{};
-
-  const int l32 = lane & 31, hi = lane >> 5;
-  const int arow = wm * 128 + l32;
-  const int wrow = wn * 128 + l32;
-  bf16x8 fa[2][4], fw[2][4];
-  auto read_frags = [&](const char* buf, int ks, bf16x8 (&a)[4], bf16x8 (&b)[4]) {
-    const int c = ks * 2 + hi;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = frag(buf, arow + t * 32, c);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) b[t] = frag(buf + kTileBytes, wrow + t * 32, c);
-  };
-  auto mma = [&](const bf16x8 (&a)[4], const bf16x8 (&b)[4]) {
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[nt][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[nt], a[mt], acc[nt][mt], 0, 0, 0);
-  };
-
   const int nk = K / BK;
-#pragma unroll
-  for (int p = 0; p < 16; ++p) stage_piece(0, 0, p);
-  wait_vmcnt0();
-  __builtin_amdgcn_s_barrier();
+  const int total = count * nk;
 
-  // One K-tile: k-step ks runs its 16 MFMAs while the fragments of ks+1 (8 ds_read_b128)
-  // and 4 of the 16 staging DMAs of K-tile t+1 are issued between them; the interleave is
-  // pinned with sched_group_barrier so that no LDS wait lands in front of an MFMA block.
-  auto ktile = [&](int t, auto pre_tag) {
-    constexpr bool kPre = decltype(pre_tag)::value;
-    const char* cur = smem + (t & 1) * kBuf;
-    const int nb = (t & 1) ^ 1;
-    read_frags(cur, 0, fa[0], fw[0]);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks < 3) read_frags(cur, ks + 1, fa[(ks + 1) & 1], fw[(ks + 1) & 1]);
-      if constexpr (kPre) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) stage_piece(nb, t + 1, ks * 4 + p);
-      }
-      mma(fa[ks & 1], fw[ks & 1]);
-      // next k-step's 8 DS reads first (other register set), then 16 MFMA with the 4 DMA
-      // issued behind the first four
-      if (ks < 3) __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (kPre) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+  // ---- staging: wave w fills pieces w*8+i (i = 0..7) of A and of W; piece = 8 rows x 128 B.
+  // Lane: row (lane>>3) of the piece, LDS chunk (lane&7) <- source chunk (lane&7)^swz(row);
+  // swz(row) of piece i depends only on i & 1.
+  const uint32_t a_rb = (uint32_t)(lda * 2), w_rb = (uint32_t)(ldw * 2);
+  const uint64_t a_bytes = (uint64_t)M * a_rb, w_bytes = (uint64_t)N * w_rb;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)(uint32_t)a_bytes, 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, (int)(uint32_t)w_bytes, 0x00020000);
+  const int prow = lane >> 3;
+  const uint32_t cE = (uint32_t)((lane & 7) ^ swz(prow)) * 16;       // even pieces
+  const uint32_t cO = (uint32_t)((lane & 7) ^ swz(prow + 8)) * 16;   // odd pieces
+  const uint32_t vA[2] = {prow * a_rb + cE, prow * a_rb + cO};
+  const uint32_t vW[2] = {prow * w_rb + cE, prow * w_rb + cO};
+  typedef __attribute__((address_space(3))) void lds_void;
+  // load stream: K-tile ld_g -> (tile ld_tm/ld_tn, K-tile ld_kt); the tail re-loads the last
+  // K-tile (harmless), so every wait count stays uniform
+  int ld_g = 0, ld_kt = 0, ld_tile = first;
+  int ld_tm = ld_tile / tilesN, ld_tn = ld_tile - ld_tm * tilesN;
+  auto advance = [&]() {
+    if (ld_g + 1 >= total) return;
+    ++ld_g;
+    if (++ld_kt == nk) {
+      ld_kt = 0;
+      ld_tile += stride;
+      ld_tm = ld_tile / tilesN;
+      ld_tn = ld_tile - ld_tm * tilesN;
     }
-    wait_vmcnt0();
-    __builtin_amdgcn_s_barrier();
   };
-  for (int t = 0; t + 1 < nk; ++t) ktile(t, std::true_type{});
-  ktile(nk - 1, std::false_type{});
-
-  // ---- epilogue: acc[nt][mt][r] = D[n = nb + nt*32 + 8*(r>>2) + 4*hi + (r&3)][m = mb + mt*32]
-  const int mb = m0 + wm * 128 + l32;
-  const int nbase = n0 + wn * 128 + 4 * hi;
-  float keep[4] = {1.f, 1.f, 1.f, 1.f};
-  if constexpr (EPI == EPI_GELU_BF16 || EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
-    if (ep.rowpad) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) keep[mt] = 1.0f - ep.rowpad[mb + mt * 32];
+  auto stage_piece = [&](int buf, int p) {  // p: 0..7 A pieces, 8..15 W pieces
+    const int i = p & 7;
+    char* dst = smem + buf * kBuf + (p >= 8 ? kOp : 0) + (w * 8 + i) * 1024;
+    if (p < 8) {
+      const uint32_t so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
+    } else {
+      const uint32_t so = (uint32_t)(ld_tn * BN + (w * 8 + i) * 8) * w_rb + ld_kt * (BK * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void*)dst, 16, vW[i & 1], so, 0, 0);
     }
+  };
+
+  // ---- fragments: 16x16x32 operand = rows (lane&15), 16-byte chunk kh*4 + (lane>>4)
+  const int frow = lane & 15;
+  int aoff[2], woff[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const int ch = ((kh * 4 + (lane >> 4)) ^ swz(frow)) * 16;
+    aoff[kh] = (wm * 128 + frow) * 128 + ch;
+    woff[kh] = kOp + (wn * 128 + frow) * 128 + ch;
   }
+  bf16x8 fa[2][8], fw[2][8];
+  auto rd = [&](int set, int buf, int q) {  // fragment q of A (q < 8) or W, k-half `set`
+    if constexpr (DIAG & 2) {
+      asm volatile("" : "+v"(fa[set][q & 7]), "+v"(fw[set][q & 7]));
+      return;
+    }
+    const char* base = smem + buf * kBuf;
+    if (q < 8) fa[set][q] = *reinterpret_cast<const bf16x8*>(base + aoff[set] + q * 2048);
+    else fw[set][q - 8] = *reinterpret_cast<const bf16x8*>(base + woff[set] + (q - 8) * 2048);
+  };
+
+  f32x4 acc[8][8];
+  // the first k-half of every tile starts its accumulators from 0 (C = inline constant)
+  auto mfma = [&](int set, int idx, bool zero) {  // idx = nt*8 + mt
+    const int nt = idx >> 3, mt = idx & 7;
+    acc[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+        fw[set][nt], fa[set][mt], zero ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[nt][mt], 0, 0, 0);
+  };
+
+  // ---- prologue: K-tiles 0, 1 into buffers 0, 1; fragments of (0, h0)
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
+  for (int p = 0; p < 16; ++p) stage_piece(0, p);
+  advance();
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int n = nbase + nt * 32 + g4 * 8;
+  for (int p = 0; p < 16; ++p) stage_piece(1, p);
+  advance();
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  sched_fence();
+  __builtin_amdgcn_s_barrier();
+  sched_fence();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) rd(0, 0, q);
+
+  // h0 of K-tile g (buffer cb): MFMAs set 0, reads of set 1 <- (g, h1)
+  auto h0 = [&](int cb, bool zero) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sched_fence();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) rd(1, cb, q);
+#pragma unroll
+    for (int idx = 0; idx < 64; ++idx) mfma(0, idx, zero);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    sched_fence();
+  };
+  // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
+  // 16 loads of K-tile g+2 into buffer cb
+  auto h1 = [&](int cb) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sched_fence();
+    mfma(1, 0, false);
+    mfma(1, 1, false);
+    sched_fence();
+    __builtin_amdgcn_s_barrier();
+    sched_fence();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      rd(0, cb ^ 1, q);
+      if constexpr (!(DIAG & 4)) stage_piece(cb, q);
+    }
+#pragma unroll
+    for (int idx = 2; idx < 64; ++idx) mfma(1, idx, false);
+#pragma unroll
+    for (int q = 0; q < 15; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    sched_fence();
+    advance();  // after the scheduled block: its branch must not split it
+  };
+
+  int g = 0;
+  for (int j = 0; j < count; ++j) {
+    h0(g & 1, true);
+    h1(g & 1);
+    ++g;
+    for (int kt = 1; kt < nk; ++kt, ++g) {
+      h0(g & 1, false);
+      h1(g & 1);
+    }
+
+    // ---- epilogue of tile j: acc[nt][mt][r] = D[n = nb + 16*nt + 4*(lane>>4) + r][m = mb + 16*mt]
+    const int tile = first + j * stride;
+    const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
+    const int mb = m0 + wm * 128 + frow;
+    const int nbase = n0 + wn * 128 + (lane >> 4) * 4;
+    using Tr = EpiTraits<EPI>;
+    float keep[8];
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) keep[mt] = 1.0f;
+    if constexpr (Tr::kKeep) {
+      if (ep.rowpad) {
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) keep[mt] = 1.0f - ep.rowpad[mb + mt * 16];
+      }
+    }
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) {
+      const int n = nbase + nt * 16;
       const float4 bb = *reinterpret_cast<const float4*>(ep.bias + n);
-      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+      float4 ex[8];  // residual / position rows, all issued before the first store
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const f32x16& a = acc[nt][mt];
-          float v0 = a[4 * g4] + bb.x, v1 = a[4 * g4 + 1] + bb.y, v2 = a[4 * g4 + 2] + bb.z,
-                v3 = a[4 * g4 + 3] + bb.w;
-          if constexpr (EPI == EPI_GELU_BF16) {
-            v0 = gelu_fast(v0) * keep[mt]; v1 = gelu_fast(v1) * keep[mt];
-            v2 = gelu_fast(v2) * keep[mt]; v3 = gelu_fast(v3) * keep[mt];
-          }
-          *reinterpret_cast<uint2*>(static_cast<bf16_t*>(ep.out) + (int64_t)(mb + mt * 32) * ep.ldo + n) =
-              make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-        }
-      } else if constexpr (EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN) {
-        float4 r[4];
+      for (int mt = 0; mt < 8; ++mt) ex[mt] = epi_extra<EPI>(ep, mb + mt * 16, n, N);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          r[mt] = *reinterpret_cast<const float4*>(ep.resid + (int64_t)(mb + mt * 32) * ep.ldr + n);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const f32x16& a = acc[nt][mt];
-          const float k = keep[mt];
-          *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)(mb + mt * 32) * ep.ldo + n) =
-              make_float4(r[mt].x + (a[4 * g4] + bb.x) * k, r[mt].y + (a[4 * g4 + 1] + bb.y) * k,
-                          r[mt].z + (a[4 * g4 + 2] + bb.z) * k, r[mt].w + (a[4 * g4 + 3] + bb.w) * k);
-        }
-      } else {  // EPI_POS_F32
-        float4 pp[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          pp[mt] = *reinterpret_cast<const float4*>(ep.pos + (int64_t)((mb + mt * 32) % ep.pos_rows) * N + n);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const f32x16& a = acc[nt][mt];
-          *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)(mb + mt * 32) * ep.ldo + n) =
-              make_float4(a[4 * g4] + bb.x + pp[mt].x, a[4 * g4 + 1] + bb.y + pp[mt].y,
-                          a[4 * g4 + 2] + bb.z + pp[mt].z, a[4 * g4 + 3] + bb.w + pp[mt].w);
-        }
+      for (int mt = 0; mt < 8; ++mt) {
+        const f32x4 a = acc[nt][mt];
+        epi_store<EPI>(ep, mb + mt * 16, n, make_float4(a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w),
+                       keep[mt], ex[mt]);
       }
     }
   }
+  // drain the tail's (clamped) loads before the workgroup's LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int EPI>
+int num_cus_w4() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int EPI, int DIAG = 0>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int grid = (M / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI>), dim3(grid), dim3(kThreads), kLds, s, A, lda, W,
+  const int tiles = (M / BM) * (N / BN);
+  const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
+  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG>), dim3(grid), dim3(kThreads), kLds, s, A, lda, W,
                      ldw, M, N, K, ep);
   return hipGetLastError();
 }
@@ -224,12 +277,27 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
 
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s) {
+  // byte offsets into A / W must fit the 32-bit buffer range
+  if ((uint64_t)M * (uint64_t)lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * (uint64_t)ldw * 2 >= 0xFFFFFFF0ull)
+    return hipErrorInvalidValue;
+  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
+  if (epi >= 1000) {  // ablation builds, EPI_BF16 epilogue
+    switch (epi - 1000) {
+      case 2: return launch_w4<EPI_BF16, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 4: return launch_w4<EPI_BF16, 4>(A, lda, W, ldw, M, N, K, ep, s);
+      case 6: return launch_w4<EPI_BF16, 6>(A, lda, W, ldw, M, N, K, ep, s);
+    }
+    return hipErrorInvalidValue;
+  }
   switch (epi) {
     case EPI_BF16: return launch_w4<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_GELU_BF16: return launch_w4<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_F32: return launch_w4<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_F32: return launch_w4<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN: return launch_w4<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_BF16: return launch_w4<EPI_POS_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16: return launch_w4<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

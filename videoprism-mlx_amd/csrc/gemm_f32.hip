@@ -34,7 +34,7 @@ __device__ __forceinline__ void epi_f32(const EpiArgs& ep, int N, int m, int n, 
       const float keep = 1.0f - ep.rowpad[m];
       v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
     }
-    const float4 r = *reinterpret_cast<const float4*>(ep.resid + (int64_t)m * ep.ldr + n);
+    const float4 r = *reinterpret_cast<const float4*>(static_cast<const float*>(ep.resid) + (int64_t)m * ep.ldr + n);
     *reinterpret_cast<float4*>(out) = make_float4(r.x + v0, r.y + v1, r.z + v2, r.w + v3);
   } else {
     const float4 p =

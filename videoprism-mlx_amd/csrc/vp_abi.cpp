@@ -288,8 +288,10 @@ WsLayout ws_layout(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t 
   const int64_t bigcols = std::max(std::max(3 * D, F), kpad);
   WsLayout L;
   size_t off = 0;
-  L.x = off; off = align256(off + (size_t)M * D * 4);
-  L.x2 = off; off = align256(off + (size_t)M * D * 4);
+  // residual streams: fp32, or bf16 when fprop_dtype is bf16 (Flax keeps activations in
+  // fprop_dtype between layers, models.py:301-302)
+  L.x = off; off = align256(off + (size_t)M * D * es);
+  L.x2 = off; off = align256(off + (size_t)M * D * es);
   L.hbuf = off; off = align256(off + (size_t)M * D * es);
   L.big = off; off = align256(off + (size_t)M * bigcols * es);
   L.pad_btn = off; off = align256(off + (size_t)M * 4);
@@ -482,8 +484,8 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   const int D = c.model_dim, F = c.mlp_dim, NH = c.num_heads;
   const size_t es = bf ? 2 : 4;
   char* ws = static_cast<char*>(workspace);
-  float* x = reinterpret_cast<float*>(ws + L.x);
-  float* x2 = reinterpret_cast<float*>(ws + L.x2);
+  void* x = ws + L.x;
+  void* x2 = ws + L.x2;
   void* hb = ws + L.hbuf;
   void* big = ws + L.big;
   float* pad_btn = nullptr;
@@ -494,14 +496,18 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
     VP_HIP(expand_paddings(frame_paddings, (int)B, (int)T, Nsp, pad_btn, pad_bnt, s));
   }
   auto gemm = [&](int epi, const void* A, int K, const void* Wt, int N, void* o, int64_t ldo,
-                  const float* bias, const float* resid, const float* pos, int pos_rows,
+                  const float* bias, const void* resid, const float* pos, int pos_rows,
                   const float* rowpad) -> hipError_t {
     EpiArgs ep;
     ep.out = o; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldo;
     ep.pos = pos; ep.pos_rows = pos_rows; ep.rowpad = rowpad;
-    if (bf) return gemm_bf16(epi, (const bf16_t*)A, K, (const bf16_t*)Wt, K, M, N, K, ep, s);
+    if (bf) return gemm_bf16_auto(epi, (const bf16_t*)A, K, (const bf16_t*)Wt, K, M, N, K, ep, s);
     return gemm_f32(epi, (const float*)A, K, (const float*)Wt, K, M, N, K, ep, s);
   };
+  // residual-stream epilogues in the stream's dtype
+  const int epi_pos = bf ? EPI_POS_BF16 : EPI_POS_F32;
+  const int epi_resid = bf ? EPI_RESID_BF16 : EPI_RESID_F32;
+  const int epi_resid_ffn = bf ? EPI_RESID_FFN_BF16 : EPI_RESID_FFN;
   const char* ge = bf ? gemm_bf16_check(M, 3 * D, D, D, D) : gemm_f32_check(M, 3 * D, D);
   if (ge) return fail(VP_ENOTSUP, ge);
   // profiled launch: records events around `fn` when vp_profile_enable() is active
@@ -525,32 +531,32 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   const double kreal = (double)P_ * P_ * 3;
   VP_HIP(rec(PC_PATCHIFY, 0.0, dM * kreal * (in_dtype == VP_BF16 ? 2 : 4) + dM * h->kpad * dE, [&] {
     return patchify(video, in_dtype == VP_BF16, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
-  VP_HIP(rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, 4, 0), [&] {
-    return gemm(EPI_POS_F32, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr, h->spatial_pos, Nsp, nullptr); }));
-  const double ln_bytes = dM * dD * 4 + dM * dD * dE;
+  VP_HIP(rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, dE, 0), [&] {
+    return gemm(epi_pos, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr, h->spatial_pos, Nsp, nullptr); }));
+  const double ln_bytes = dM * dD * dE + dM * dD * dE;
 
-  auto run_stack = [&](std::vector<LayerW>& layers, float* xs, int num_seq, int S,
+  auto run_stack = [&](std::vector<LayerW>& layers, void* xs, int num_seq, int S,
                        const float* pad) -> int {
     const int acls = num_seq == (int)(B * T) ? PC_ATTN_SPATIAL : PC_ATTN_TEMPORAL;
     const double aflops = 4.0 * num_seq * (double)S * S * dD;
     const double abytes = dM * 3 * dD * dE + dM * dD * dE;
     for (auto& lw : layers) {
       VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
-        return layernorm(xs, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
+        return layernorm(xs, bf, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
       VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
         return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
       VP_HIP(rec(acls, aflops, abytes, [&] {
         if (!bf) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s);
         if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, c.atten_logit_cap, pad, s);
         return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s); }));
-      VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, 4, 4), [&] {
-        return gemm(EPI_RESID_F32, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1, nullptr); }));
+      VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {
+        return gemm(epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1, nullptr); }));
       VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
-        return layernorm(xs, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
+        return layernorm(xs, bf, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
       VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
         return gemm(EPI_GELU_BF16, hb, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad); }));
-      VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, 4, 4), [&] {
-        return gemm(EPI_RESID_FFN, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1, pad); }));
+      VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, dE, dE), [&] {
+        return gemm(epi_resid_ffn, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1, pad); }));
     }
     return VP_OK;
   };
@@ -558,16 +564,16 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   if ((rc = run_stack(h->spatial, x, (int)(B * T), Nsp, pad_btn))) return rc;
   // 3. spatial_ln (+ optional spatial_features), transpose to (b n) t, + temporal pos-emb
   if (spatial_out)
-    VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * 4 + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
-      return layernorm(x, M, D, h->sln_g, h->sln_b, spatial_out, out_dtype == VP_BF16, PERM_NONE, 1, 1, nullptr, s); }));
+    VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * dE + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
+      return layernorm(x, bf, M, D, h->sln_g, h->sln_b, spatial_out, out_dtype == VP_BF16, PERM_NONE, 1, 1, nullptr, s); }));
   const float* tpos = h->temporal_pos + (size_t)T * kMaxT * D;
-  VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * 8, [&] {
-    return layernorm(x, M, D, h->sln_g, h->sln_b, x2, 0, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s); }));
+  VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
+    return layernorm(x, bf, M, D, h->sln_g, h->sln_b, x2, bf, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s); }));
   // 4. temporal encoder over (b n) sequences of T tokens
   if ((rc = run_stack(h->temporal, x2, (int)(B * Nsp), (int)T, pad_bnt))) return rc;
   // 5. temporal_ln and '(bn)td->b(tn)d'
-  VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * 4 + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
-    return layernorm(x2, M, D, h->tln_g, h->tln_b, out, out_dtype == VP_BF16, PERM_BNT_TO_BTN, (int)T, Nsp, nullptr, s); }));
+  VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * dE + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
+    return layernorm(x2, bf, M, D, h->tln_g, h->tln_b, out, out_dtype == VP_BF16, PERM_BNT_TO_BTN, (int)T, Nsp, nullptr, s); }));
   (void)es;
   return VP_OK;
 }
@@ -622,13 +628,17 @@ int vp_profile_class_count(void) { return PC_COUNT; }
 
 int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const void* W, int64_t ldw,
                int64_t M, int64_t N, int64_t K, void* out, int64_t ldo, const float* bias,
-               const float* resid, int64_t ldr, const float* pos, int64_t pos_rows,
+               const void* resid, int64_t ldr, const float* pos, int64_t pos_rows,
                const float* rowpad, void* stream) {
   using namespace vp;
   if (!A || !W || !out || !bias) return fail(VP_EINVAL, "null argument");
-  if (epilogue < 0 || epilogue > 4) return fail(VP_EINVAL, "bad epilogue");
-  if ((epilogue == EPI_RESID_F32 || epilogue == EPI_RESID_FFN) && !resid) return fail(VP_EINVAL, "resid required");
-  if (epilogue == EPI_POS_F32 && (!pos || pos_rows < 1)) return fail(VP_EINVAL, "pos required");
+  if (epilogue < 0 || epilogue > 7) return fail(VP_EINVAL, "bad epilogue");
+  const bool needs_resid = epilogue == EPI_RESID_F32 || epilogue == EPI_RESID_FFN ||
+                           epilogue == EPI_RESID_BF16 || epilogue == EPI_RESID_FFN_BF16;
+  if (needs_resid && !resid) return fail(VP_EINVAL, "resid required");
+  if ((epilogue == EPI_POS_F32 || epilogue == EPI_POS_BF16) && (!pos || pos_rows < 1))
+    return fail(VP_EINVAL, "pos required");
+  if (precision == VP_F32 && epilogue > 4) return fail(VP_EINVAL, "bf16 residual epilogues need precision VP_BF16");
   EpiArgs ep;
   ep.out = out; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldr;
   ep.pos = pos; ep.pos_rows = (int)pos_rows; ep.rowpad = rowpad;
@@ -636,7 +646,7 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
   if (precision == VP_BF16) {
     const char* e = gemm_bf16_check((int)M, (int)N, (int)K, lda, ldw);
     if (e) return fail(VP_EINVAL, e);
-    VP_HIP(gemm_bf16(epilogue, (const bf16_t*)A, lda, (const bf16_t*)W, ldw, (int)M, (int)N, (int)K, ep, s));
+    VP_HIP(gemm_bf16_auto(epilogue, (const bf16_t*)A, lda, (const bf16_t*)W, ldw, (int)M, (int)N, (int)K, ep, s));
   } else if (precision == VP_F32) {
     const char* e = gemm_f32_check((int)M, (int)N, (int)K);
     if (e) return fail(VP_EINVAL, e);
@@ -660,16 +670,25 @@ int vp_dev_gemm_diag(int diag, const void* A, const void* W, int64_t M, int64_t 
   return VP_OK;
 }
 
-// Not in the public header: the 4-wave bf16 GEMM with any epilogue (tools/gemm_bench.py).
-int vp_dev_gemm_w4(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K,
-                   void* out, const float* bias, const float* resid, void* stream) {
+// Not in the public header: one named bf16 GEMM kernel (which = 4: gemm_bf16_w4, 8: gemm_bf16)
+// with any epilogue, for kernel A/B tests (tests/test_gpu_kernels.py) and tools/gemm_bench.py.
+// epi >= 1000 selects the 4-wave kernel's ablation builds.
+int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t M, int64_t N,
+                       int64_t K, void* out, const float* bias, const void* resid, const float* pos,
+                       int64_t pos_rows, const float* rowpad, void* stream) {
   using namespace vp;
   const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
-  VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
-                      static_cast<hipStream_t>(stream)));
+  ep.pos = pos; ep.pos_rows = (int)(pos_rows > 0 ? pos_rows : 1); ep.rowpad = rowpad;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (which == 4)
+    VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
+  else if (which == 8)
+    VP_HIP(gemm_bf16(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
+  else
+    return fail(VP_EINVAL, "which must be 4 or 8");
   return VP_OK;
 }
 
@@ -695,14 +714,16 @@ int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, in
   return VP_OK;
 }
 
-int vp_op_layernorm(const float* x, int64_t rows, int64_t D, const float* gamma, const float* beta,
-                    void* out, int out_dtype, int perm, int64_t T, int64_t Nsp, const float* add,
-                    void* stream) {
+int vp_op_layernorm(const void* x, int in_dtype, int64_t rows, int64_t D, const float* gamma,
+                    const float* beta, void* out, int out_dtype, int perm, int64_t T, int64_t Nsp,
+                    const float* add, void* stream) {
   using namespace vp;
   if (!x || !gamma || !beta || !out) return fail(VP_EINVAL, "null argument");
+  if ((in_dtype != VP_F32 && in_dtype != VP_BF16) || (out_dtype != VP_F32 && out_dtype != VP_BF16))
+    return fail(VP_EINVAL, "bad dtype");
   if (perm && (T < 1 || Nsp < 1 || rows % (T * Nsp))) return fail(VP_EINVAL, "bad permutation geometry");
-  hipError_t e = layernorm(x, (int)rows, (int)D, gamma, beta, out, out_dtype == VP_BF16, perm,
-                           (int)T, (int)Nsp, add, static_cast<hipStream_t>(stream));
+  hipError_t e = layernorm(x, in_dtype == VP_BF16, (int)rows, (int)D, gamma, beta, out, out_dtype == VP_BF16,
+                           perm, (int)T, (int)Nsp, add, static_cast<hipStream_t>(stream));
   if (e == hipErrorInvalidValue) return fail(VP_ENOTSUP, "layernorm: D must be 256*k, k in {1..6, 8}");
   VP_HIP(e);
   return VP_OK;

@@ -14,13 +14,17 @@ enum Epilogue {
   EPI_RESID_F32 = 2,  // out_f32  = resid + (acc + bias) * (1 - rowpad)   (post, ffn_layer2)
   EPI_POS_F32 = 3,    // out_f32  = acc + bias + pos[m % pos_rows]   (patch_projection + pos emb)
   EPI_RESID_FFN = 4,  // = EPI_RESID_F32, separate kernel symbol for ffn_layer2 (profiling)
+  // bf16 residual stream (bf16 GEMM only): same as 2 / 3 / 4 with bf16 resid and output
+  EPI_RESID_BF16 = 5,
+  EPI_POS_BF16 = 6,
+  EPI_RESID_FFN_BF16 = 7,
 };
 
 struct EpiArgs {
   void* out = nullptr;
   int64_t ldo = 0;
   const float* bias = nullptr;    // [N]
-  const float* resid = nullptr;   // EPI_RESID_F32 (may alias out)
+  const void* resid = nullptr;    // EPI_RESID_*: fp32 or bf16 by epilogue (may alias out)
   int64_t ldr = 0;
   const float* pos = nullptr;     // EPI_POS_F32: [pos_rows][N]
   int pos_rows = 1;
@@ -32,9 +36,13 @@ const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw);
 hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                      int N, int K, const EpiArgs& ep, hipStream_t s);
 
-// 4-wave (one wave per SIMD, 128x128 per wave, 32x32x16 MFMA) decomposition
+// 4-wave (one wave per SIMD, 128x128 per wave, 16x16x32 MFMA, full-line buffer_load..lds
+// staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
+// picks gemm_bf16_w4 or gemm_bf16 by shape (VP_GEMM_KERNEL=w8|w4 overrides)
+hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                          int N, int K, const EpiArgs& ep, hipStream_t s);
 
 // ablation builds of the bf16 GEMM (store epilogue) for tools/gemm_bench.py
 hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
@@ -60,11 +68,11 @@ enum RowPerm { PERM_NONE = 0, PERM_BTN_TO_BNT = 1, PERM_BNT_TO_BTN = 2 };
 // video [BT, H, W, C] (f32 or bf16) -> patches [BT*np, kpad] (bf16 or f32), zero-padded K.
 hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is_bf16, int BT,
                     int H, int W, int C, int P, int kpad, hipStream_t s);
-// LayerNorm over D of fp32 rows; gamma already holds (1 + scale).  Output row r goes to
-// row perm(r); `add` (optional, fp32 [add_rows][D]) is added by the *output* row's t index.
-hipError_t layernorm(const float* x, int rows, int D, const float* gamma, const float* beta,
-                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add,
-                     hipStream_t s);
+// LayerNorm over D of fp32 or bf16 rows; gamma already holds (1 + scale).  Output row r goes
+// to row perm(r); `add` (optional, fp32 [add_rows][D]) is added by the *output* row's t index.
+hipError_t layernorm(const void* x, int in_is_bf16, int rows, int D, const float* gamma,
+                     const float* beta, void* out, int out_is_bf16, int perm, int T, int Nsp,
+                     const float* add, hipStream_t s);
 // fp32 -> bf16 cast (weights are pre-packed on the host; this is for activations)
 hipError_t cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s);
 // per-token padding vector expansion: frame_pad [B*T] -> token pads in both orders

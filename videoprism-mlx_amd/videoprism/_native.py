@@ -18,6 +18,8 @@ VP_OK, VP_EINVAL, VP_ENOMEM, VP_EHIP, VP_ESTATE, VP_ENOTSUP = range(6)
 VP_F32, VP_BF16 = 0, 1
 
 EPI_STORE, EPI_GELU, EPI_RESID, EPI_POS, EPI_RESID_FFN = 0, 1, 2, 3, 4
+# bf16 residual stream variants (bf16 resid / out; bf16 precision only)
+EPI_RESID_BF16, EPI_POS_BF16, EPI_RESID_FFN_BF16 = 5, 6, 7
 PERM_NONE, PERM_BTN_TO_BNT, PERM_BNT_TO_BTN = 0, 1, 2
 
 
@@ -70,11 +72,15 @@ _SIGNATURES = {
                            c_int64, c_void_p, c_void_p]),
     "vp_op_attention": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
                                 c_void_p, c_void_p]),
-    "vp_op_layernorm": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int,
-                                c_int, c_int64, c_int64, c_void_p, c_void_p]),
+    "vp_op_layernorm": (c_int, [c_void_p, c_int, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                c_int, c_int, c_int64, c_int64, c_void_p, c_void_p]),
     "vp_op_patchify": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64,
                                c_int64, c_int64, c_void_p]),
     "vp_op_pool_l2": (c_int, [c_void_p, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+    # not in the public header: named-kernel GEMM for A/B tests and tools/gemm_bench.py
+    "vp_dev_gemm_kernel": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                   c_void_p]),
 }
 
 _lib = None
@@ -152,12 +158,24 @@ def op_gemm(a, w, bias, epilogue=EPI_STORE, out=None, resid=None, pos=None, rowp
     M, K = a.shape
     N = w.shape[0]
     if out is None:
-        odt = a.dtype if epilogue in (EPI_STORE, EPI_GELU) else torch.float32
+        odt = (a.dtype if epilogue in (EPI_STORE, EPI_GELU) else
+               torch.bfloat16 if epilogue >= EPI_RESID_BF16 else torch.float32)
         out = torch.empty((M, N), dtype=odt, device=a.device)
     call("vp_op_gemm", _prec(a), epilogue, _ptr(a), a.stride(0), _ptr(w), w.stride(0), M, N, K,
          _ptr(out), out.stride(0), _ptr(bias), _ptr(resid),
          resid.stride(0) if resid is not None else 0, _ptr(pos),
          pos.shape[0] if pos is not None else 0, _ptr(rowpad), _stream(stream))
+    return out
+
+
+def dev_gemm_kernel(which, a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None,
+                    stream=None):
+    """bf16 GEMM through one named kernel (4 = 4-wave, 8 = 8-wave); out/resid contiguous."""
+    M, K = a.shape
+    N = w.shape[0]
+    call("vp_dev_gemm_kernel", which, epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias),
+         _ptr(resid), _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad),
+         _stream(stream))
     return out
 
 
@@ -177,7 +195,7 @@ def op_layernorm(x, gamma1p, beta, out_dtype=None, perm=PERM_NONE, T=1, Nsp=1, a
     rows, D = x.shape
     out_dtype = out_dtype or torch.float32
     out = torch.empty((rows, D), dtype=out_dtype, device=x.device)
-    call("vp_op_layernorm", _ptr(x), rows, D, _ptr(gamma1p), _ptr(beta), _ptr(out),
+    call("vp_op_layernorm", _ptr(x), _prec(x), rows, D, _ptr(gamma1p), _ptr(beta), _ptr(out),
          VP_BF16 if out_dtype == torch.bfloat16 else VP_F32, perm, T, Nsp, _ptr(add),
          _stream(stream))
     return out
