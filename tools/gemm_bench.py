@@ -23,6 +23,7 @@ SHAPES = [  # name, M, N, K, epilogue (as in vp_forward's bf16 path)
     ("ffn1", M_TOK, 3072, 768, nat.EPI_GELU),
     ("ffn2", M_TOK, 768, 3072, nat.EPI_RESID_FFN_BF16),
 ]
+EXTRA = [("ffn1-noact", M_TOK, 3072, 768, nat.EPI_STORE)]  # prices the GELU epilogue
 
 
 def timeit(fn, iters=20, warm=3):
@@ -46,7 +47,7 @@ def operands(M, N, K, g, dev):
 
 
 def compare(dev, g):
-    for name, M, N, K, epi in SHAPES:
+    for name, M, N, K, epi in SHAPES + EXTRA:
         a, w, b = operands(M, N, K, g, dev)
         resid = epi in (nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16)
         x0 = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16) if resid else None
@@ -101,7 +102,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
     if mode == "w4var":
-        variants(dev, g, 4, [0, 2, 4, 6])
+        variants(dev, g, 4, [0, 4, 6, 8, 14])
     elif mode == "w8var":
         variants(dev, g, 8, [0, 1, 2, 8, 16])
     else:

@@ -34,6 +34,10 @@ constexpr int kThreads = 256;
 constexpr int kOp = BM * BK * 2;             // 32 KiB: one operand's K-tile
 constexpr int kBuf = 2 * kOp;                // A then W
 constexpr int kLds = 2 * kBuf;               // 128 KiB
+// per-wave epilogue scratch: 16 rows x 64 fp32 columns, rows padded by 16 B (bank spread)
+constexpr int kScrRow = 64 * 4 + 16;
+constexpr int kScr = 16 * kScrRow;           // 4352 B
+constexpr int kLdsTotal = kLds + 4 * kScr;   // 148480 B
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -41,7 +45,8 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
 // DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 2 = no ds_reads
-// in the K loop, 4 = no staging loads after the prologue.
+// in the K loop, 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at
+// run time; the accumulators stay live).
 template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -211,33 +216,62 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       h1(g & 1);
     }
 
-    // ---- epilogue of tile j: acc[nt][mt][r] = D[n = nb + 16*nt + 4*(lane>>4) + r][m = mb + 16*mt]
-    const int tile = first + j * stride;
-    const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
-    const int mb = m0 + wm * 128 + frow;
-    const int nbase = n0 + wn * 128 + (lane >> 4) * 4;
-    using Tr = EpiTraits<EPI>;
-    float keep[8];
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) keep[mt] = 1.0f;
-    if constexpr (Tr::kKeep) {
-      if (ep.rowpad) {
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) keep[mt] = 1.0f - ep.rowpad[mb + mt * 16];
-      }
+    // ---- epilogue of tile j.  acc[nt][mt] holds D[row mb + 16*mt][cols nb + 16*nt + 4*(lane>>4)
+    // + 0..3] (row mb = m0 + wm*128 + (lane&15)).  Each 16-row x 64-column block goes through the
+    // wave's LDS scratch so that a lane owns 8 consecutive columns of one row: every store and
+    // residual load instruction then covers 8 rows x 128 B (bf16) -- full lines instead of
+    // 16 rows x 32 B.  Same fp32 math and single rounding as the direct epilogue.
+    if constexpr (DIAG & 8) {
+      if (ep.ldo != -12345) continue;  // never false at run time: keeps acc live, skips stores
     }
+    const int tile = first + j * stride;
+    const int m0 = (tile / tilesN) * BM + wm * 128, n0 = (tile % tilesN) * BN + wn * 128;
+    using Tr = EpiTraits<EPI>;
+    char* scr = smem + kLds + w * kScr;
+    const int er = lane >> 3, es = lane & 7;  // read-back: row pass*8 + er, column segment es
+    float4 bl[2], bh[2];
 #pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      const int n = nbase + nt * 16;
-      const float4 bb = *reinterpret_cast<const float4*>(ep.bias + n);
-      float4 ex[8];  // residual / position rows, all issued before the first store
+    for (int nh = 0; nh < 2; ++nh) {
+      bl[nh] = *reinterpret_cast<const float4*>(ep.bias + n0 + nh * 64 + es * 8);
+      bh[nh] = *reinterpret_cast<const float4*>(ep.bias + n0 + nh * 64 + es * 8 + 4);
+    }
+    // residual / position rows of block mt+1 are requested before block mt's stores, so a
+    // load never waits behind the stores just issued (vmcnt retires in issue order)
+    F8 ex[2][2][2];  // [buffer][nh][pass]
+    auto fetch = [&](int b, int mt) {
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) ex[mt] = epi_extra<EPI>(ep, mb + mt * 16, n, N);
+      for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        const f32x4 a = acc[nt][mt];
-        epi_store<EPI>(ep, mb + mt * 16, n, make_float4(a[0] + bb.x, a[1] + bb.y, a[2] + bb.z, a[3] + bb.w),
-                       keep[mt], ex[mt]);
+        for (int pass = 0; pass < 2; ++pass)
+          ex[b][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+    };
+    if constexpr (Tr::kExtra) fetch(0, 0);
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      if constexpr (Tr::kExtra) {
+        if (mt < 7) fetch((mt + 1) & 1, mt + 1);
+      }
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(scr + frow * kScrRow + (q * 16 + (lane >> 4) * 4) * 4) = acc[nh * 4 + q][mt];
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const int rl = pass * 8 + er;
+          const int row = m0 + mt * 16 + rl;
+          const int n = n0 + nh * 64 + es * 8;
+          F8 v;
+          v.lo = *reinterpret_cast<const float4*>(scr + rl * kScrRow + es * 32);
+          v.hi = *reinterpret_cast<const float4*>(scr + rl * kScrRow + es * 32 + 16);
+          v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
+          v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
+          float keep = 1.0f;
+          if constexpr (Tr::kKeep) {
+            if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
+          }
+          epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+        }
       }
     }
   }
@@ -262,13 +296,13 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
-  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG>), dim3(grid), dim3(kThreads), kLds, s, A, lda, W,
+  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
                      ldw, M, N, K, ep);
   return hipGetLastError();
 }
@@ -286,6 +320,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 2: return launch_w4<EPI_BF16, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 4: return launch_w4<EPI_BF16, 4>(A, lda, W, ldw, M, N, K, ep, s);
       case 6: return launch_w4<EPI_BF16, 6>(A, lda, W, ldw, M, N, K, ep, s);
+      case 8: return launch_w4<EPI_BF16, 8>(A, lda, W, ldw, M, N, K, ep, s);
+      case 14: return launch_w4<EPI_BF16, 14>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
   }

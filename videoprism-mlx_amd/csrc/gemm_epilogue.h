@@ -40,6 +40,30 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * fmaf(ax, fmaf(-p, e, 1.0f), x);
 }
 
+// The same operation sequence on two values with packed fp32 math (v_pk_fma_f32 /
+// v_pk_mul_f32): bit-identical to two gelu_fast calls, half the VALU issue slots.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t x) {
+  const f32x2_t ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2_t d = __builtin_elementwise_fma(f32x2_t(0.3275911f * 0.70710678118654752f), ax, f32x2_t(1.0f));
+  const f32x2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2_t p = __builtin_elementwise_fma(t, f32x2_t(1.061405429f), f32x2_t(-1.453152027f));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(1.421413741f));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(-0.284496736f));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(0.254829592f));
+  p = p * t;
+  const f32x2_t q = x * x * f32x2_t(-0.5f * 1.4426950408889634f);
+  const f32x2_t e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2_t erf_abs = __builtin_elementwise_fma(-p, e, f32x2_t(1.0f));
+  return f32x2_t(0.5f) * __builtin_elementwise_fma(ax, erf_abs, x);
+}
+
+__device__ __forceinline__ float4 gelu4(float4 v) {
+  const f32x2_t a = gelu_fast2(f32x2_t{v.x, v.y});
+  const f32x2_t b = gelu_fast2(f32x2_t{v.z, v.w});
+  return make_float4(a.x, a.y, b.x, b.y);
+}
+
 __device__ __forceinline__ float4 bf16x4_to_f32(uint2 u) {
   return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
@@ -66,9 +90,7 @@ template <int EPI>
 __device__ __forceinline__ void epi_store(const EpiArgs& ep, int row, int n, float4 v, float keep,
                                           float4 extra) {
   using Tr = EpiTraits<EPI>;
-  if constexpr (Tr::kGelu) {
-    v.x = gelu_fast(v.x); v.y = gelu_fast(v.y); v.z = gelu_fast(v.z); v.w = gelu_fast(v.w);
-  }
+  if constexpr (Tr::kGelu) v = gelu4(v);
   if constexpr (Tr::kKeep) {
     v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep;
   }
@@ -80,6 +102,57 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ep, int row, int n, flo
         make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
   } else {
     *reinterpret_cast<float4*>(static_cast<float*>(ep.out) + (int64_t)row * ep.ldo + n) = v;
+  }
+}
+
+// ---- 8-column forms: a lane owns columns n..n+7 of one row (LDS-transposed epilogue) ----
+struct F8 {
+  float4 lo, hi;
+};
+
+template <int EPI>
+__device__ __forceinline__ F8 epi_extra8(const EpiArgs& ep, int row, int n, int N) {
+  using Tr = EpiTraits<EPI>;
+  F8 e;
+  if constexpr (Tr::kResidF32) {
+    const float* r = static_cast<const float*>(ep.resid) + (int64_t)row * ep.ldr + n;
+    e.lo = *reinterpret_cast<const float4*>(r);
+    e.hi = *reinterpret_cast<const float4*>(r + 4);
+  } else if constexpr (Tr::kResidBf16) {
+    const uint4 u = *reinterpret_cast<const uint4*>(static_cast<const bf16_t*>(ep.resid) + (int64_t)row * ep.ldr + n);
+    e.lo = bf16x4_to_f32(make_uint2(u.x, u.y));
+    e.hi = bf16x4_to_f32(make_uint2(u.z, u.w));
+  } else if constexpr (Tr::kPos) {
+    const float* p = ep.pos + (int64_t)(row % ep.pos_rows) * N + n;
+    e.lo = *reinterpret_cast<const float4*>(p);
+    e.hi = *reinterpret_cast<const float4*>(p + 4);
+  } else {
+    e.lo = e.hi = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  return e;
+}
+
+__device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, bool gelu, bool kp, bool ex) {
+  if (gelu) v = gelu4(v);
+  if (kp) { v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep; }
+  if (ex) { v.x += extra.x; v.y += extra.y; v.z += extra.z; v.w += extra.w; }
+  return v;
+}
+
+// v = acc + bias (8 columns); same math and single rounding as epi_store
+template <int EPI>
+__device__ __forceinline__ void epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
+  using Tr = EpiTraits<EPI>;
+  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra);
+  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra);
+  if constexpr (Tr::kOutBf16) {
+    *reinterpret_cast<uint4*>(static_cast<bf16_t*>(ep.out) + (int64_t)row * ep.ldo + n) =
+        make_uint4(pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
+                   pack_bf16x2(v.hi.z, v.hi.w));
+  } else {
+    float* o = static_cast<float*>(ep.out) + (int64_t)row * ep.ldo + n;
+    *reinterpret_cast<float4*>(o) = v.lo;
+    *reinterpret_cast<float4*>(o + 4) = v.hi;
   }
 }
 
