@@ -50,9 +50,11 @@ __global__ __launch_bounds__(256) void patchify_kernel(const TI* __restrict__ vi
   }
 }
 
-// ---- LayerNorm (layers.py:208-270) over fp32 or bf16 rows, one wave per row ----
-// NCH = D / 256 4-element chunks per lane.  gamma = 1 + scale (folded on the host).
-template <int NCH, bool OUT_BF16, bool IN_BF16>
+// ---- LayerNorm (layers.py:208-270) over fp32 or bf16 rows ----
+// One wave owns RPW rows: all RPW x NCH loads are issued before the first reduction (memory-level
+// parallelism for an HBM-bound kernel), and the RPW row reductions interleave.  NCH = D / 256
+// 4-element chunks per lane.  gamma = 1 + scale (folded on the host).
+template <int NCH, bool OUT_BF16, bool IN_BF16, int RPW>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ x, int rows,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
@@ -60,67 +62,93 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
                                                         int Nsp, const float* __restrict__ add) {
   constexpr int D = NCH * 256;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  float4 v[NCH];
-  float s = 0.f;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  float4 v[RPW][NCH];
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    if constexpr (IN_BF16) {
-      const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(x) + (int64_t)row * D +
-                                                      c * 256 + lane * 4);
-      v[c] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                         __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-    } else {
-      v[c] = *reinterpret_cast<const float4*>(static_cast<const float*>(x) + (int64_t)row * D + c * 256 +
-                                              lane * 4);
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r < rows ? row0 + r : rows - 1;  // tail rows: recomputed, not stored
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      if constexpr (IN_BF16) {
+        const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(x) + (int64_t)row * D +
+                                                        c * 256 + lane * 4);
+        v[r][c] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                              __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      } else {
+        v[r][c] = *reinterpret_cast<const float4*>(static_cast<const float*>(x) + (int64_t)row * D + c * 256 +
+                                                   lane * 4);
+      }
     }
-    s += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+  }
+  float s[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    s[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) s[r] += (v[r][c].x + v[r][c].y) + (v[r][c].z + v[r][c].w);
   }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-  const float mean = s * (1.0f / D);
-  float ss = 0.f;
+  for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    v[c].x -= mean; v[c].y -= mean; v[c].z -= mean; v[c].w -= mean;
-    ss += (v[c].x * v[c].x + v[c].y * v[c].y) + (v[c].z * v[c].z + v[c].w * v[c].w);
+    for (int r = 0; r < RPW; ++r) s[r] += __shfl_xor(s[r], off);
+  float ss[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const float mean = s[r] * (1.0f / D);
+    ss[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      v[r][c].x -= mean; v[r][c].y -= mean; v[r][c].z -= mean; v[r][c].w -= mean;
+      ss[r] += (v[r][c].x * v[r][c].x + v[r][c].y * v[r][c].y) + (v[r][c].z * v[r][c].z + v[r][c].w * v[r][c].w);
+    }
   }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off);
-  const float rstd = 1.0f / sqrtf(ss * (1.0f / D) + 1e-6f);
+  for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) ss[r] += __shfl_xor(ss[r], off);
 
-  int64_t orow = row;
-  int t_of_out = 0;
-  if (perm == PERM_BTN_TO_BNT) {  // r = (b*T + t)*Nsp + n  ->  (b*Nsp + n)*T + t
-    const int n = row % Nsp;
-    const int bt = row / Nsp;
-    const int t = bt % T, b = bt / T;
-    orow = ((int64_t)b * Nsp + n) * T + t;
-    t_of_out = t;
-  } else if (perm == PERM_BNT_TO_BTN) {  // r = (b*Nsp + n)*T + t  ->  (b*T + t)*Nsp + n
-    const int t = row % T;
-    const int bn = row / T;
-    const int n = bn % Nsp, b = bn / Nsp;
-    orow = ((int64_t)b * T + t) * Nsp + n;
-    t_of_out = t;
-  }
+  float4 gm[NCH], bt[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int col = c * 256 + lane * 4;
-    const float4 gm = *reinterpret_cast<const float4*>(gamma + col);
-    const float4 bt = *reinterpret_cast<const float4*>(beta + col);
-    float4 y = make_float4(v[c].x * rstd * gm.x + bt.x, v[c].y * rstd * gm.y + bt.y,
-                           v[c].z * rstd * gm.z + bt.z, v[c].w * rstd * gm.w + bt.w);
-    if (add) {
-      const float4 a = *reinterpret_cast<const float4*>(add + (int64_t)t_of_out * D + col);
-      y.x += a.x; y.y += a.y; y.z += a.z; y.w += a.w;
+    gm[c] = *reinterpret_cast<const float4*>(gamma + c * 256 + lane * 4);
+    bt[c] = *reinterpret_cast<const float4*>(beta + c * 256 + lane * 4);
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    if (row >= rows) break;
+    const float rstd = 1.0f / sqrtf(ss[r] * (1.0f / D) + 1e-6f);
+    int64_t orow = row;
+    int t_of_out = 0;
+    if (perm == PERM_BTN_TO_BNT) {  // r = (b*T + t)*Nsp + n  ->  (b*Nsp + n)*T + t
+      const int n = row % Nsp;
+      const int btx = row / Nsp;
+      const int t = btx % T, b = btx / T;
+      orow = ((int64_t)b * Nsp + n) * T + t;
+      t_of_out = t;
+    } else if (perm == PERM_BNT_TO_BTN) {  // r = (b*Nsp + n)*T + t  ->  (b*T + t)*Nsp + n
+      const int t = row % T;
+      const int bn = row / T;
+      const int n = bn % Nsp, b = bn / Nsp;
+      orow = ((int64_t)b * T + t) * Nsp + n;
+      t_of_out = t;
     }
-    if constexpr (OUT_BF16) {
-      *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + orow * D + col) =
-          make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
-    } else {
-      *reinterpret_cast<float4*>(static_cast<float*>(out) + orow * D + col) = y;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      float4 y = make_float4(v[r][c].x * rstd * gm[c].x + bt[c].x, v[r][c].y * rstd * gm[c].y + bt[c].y,
+                             v[r][c].z * rstd * gm[c].z + bt[c].z, v[r][c].w * rstd * gm[c].w + bt[c].w);
+      if (add) {
+        const float4 a = *reinterpret_cast<const float4*>(add + (int64_t)t_of_out * D + col);
+        y.x += a.x; y.y += a.y; y.z += a.z; y.w += a.w;
+      }
+      if constexpr (OUT_BF16) {
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + orow * D + col) =
+            make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+      } else {
+        *reinterpret_cast<float4*>(static_cast<float*>(out) + orow * D + col) = y;
+      }
     }
   }
 }
@@ -188,20 +216,21 @@ int grid_for(int64_t work, int block) {
 template <int NCH>
 hipError_t ln_launch(const void* x, int in_is_bf16, int rows, const float* gamma, const float* beta,
                      void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add, hipStream_t s) {
-  const dim3 grid((rows + 3) / 4);
+  constexpr int RPW = NCH <= 4 ? 4 : 2;  // rows per wave
+  const dim3 grid((rows + 4 * RPW - 1) / (4 * RPW));
   if (in_is_bf16) {
     if (out_is_bf16)
-      hipLaunchKernelGGL((layernorm_kernel<NCH, true, true>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+      hipLaunchKernelGGL((layernorm_kernel<NCH, true, true, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
                          out, perm, T, Nsp, add);
     else
-      hipLaunchKernelGGL((layernorm_kernel<NCH, false, true>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+      hipLaunchKernelGGL((layernorm_kernel<NCH, false, true, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
                          out, perm, T, Nsp, add);
   } else {
     if (out_is_bf16)
-      hipLaunchKernelGGL((layernorm_kernel<NCH, true, false>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+      hipLaunchKernelGGL((layernorm_kernel<NCH, true, false, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
                          out, perm, T, Nsp, add);
     else
-      hipLaunchKernelGGL((layernorm_kernel<NCH, false, false>), grid, dim3(256), 0, s, x, rows, gamma, beta,
+      hipLaunchKernelGGL((layernorm_kernel<NCH, false, false, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
                          out, perm, T, Nsp, add);
   }
   return hipGetLastError();

@@ -46,7 +46,11 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 
 // DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 2 = no ds_reads
 // in the K loop, 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at
-// run time; the accumulators stay live).
+// run time; the accumulators stay live), 16 = after an epilogue the next barrier waits vmcnt(32)
+// (lets the stores drain behind the next tile; correct, measured no faster), 32 = epilogue
+// without its global stores (LDS transposition and math kept), 64 = start skew: workgroup
+// group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
+// K-tile, so the tiles' epilogue store bursts do not coincide across the chip.
 template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -174,9 +178,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   };
   // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
   // 16 loads of K-tile g+2 into buffer cb
-  auto h1 = [&](int cb) {
+  // after_epi (DIAG 16): the tile's epilogue issued >= 32 VMEM ops (its stores) after the
+  // K-stream loads this barrier needs, so vmcnt(32) retires those loads and lets the stores
+  // drain behind the next tile's MFMAs
+  auto h1 = [&](int cb, bool after_epi) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (after_epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sched_fence();
     mfma(1, 0, false);
     mfma(1, 1, false);
@@ -207,13 +215,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   };
 
   int g = 0;
+  if constexpr (DIAG & 64) {
+    const uint64_t ticks = (uint64_t)((b >> 3) & 3) * nk * 50;  // s_memrealtime runs at 100 MHz
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+  }
   for (int j = 0; j < count; ++j) {
     h0(g & 1, true);
-    h1(g & 1);
+    h1(g & 1, (DIAG & 16) && j > 0);
     ++g;
     for (int kt = 1; kt < nk; ++kt, ++g) {
       h0(g & 1, false);
-      h1(g & 1);
+      h1(g & 1, false);
     }
 
     // ---- epilogue of tile j.  acc[nt][mt] holds D[row mb + 16*mt][cols nb + 16*nt + 4*(lane>>4)
@@ -270,7 +283,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           if constexpr (Tr::kKeep) {
             if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
           }
-          epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          if constexpr (DIAG & 32) {
+            if (ep.ldo == -12345) epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+            else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
+          } else {
+            epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          }
         }
       }
     }
@@ -322,6 +340,10 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 6: return launch_w4<EPI_BF16, 6>(A, lda, W, ldw, M, N, K, ep, s);
       case 8: return launch_w4<EPI_BF16, 8>(A, lda, W, ldw, M, N, K, ep, s);
       case 14: return launch_w4<EPI_BF16, 14>(A, lda, W, ldw, M, N, K, ep, s);
+      case 16: return launch_w4<EPI_BF16, 16>(A, lda, W, ldw, M, N, K, ep, s);
+      case 32: return launch_w4<EPI_BF16, 32>(A, lda, W, ldw, M, N, K, ep, s);
+      case 64: return launch_w4<EPI_BF16, 64>(A, lda, W, ldw, M, N, K, ep, s);
+      case 80: return launch_w4<EPI_BF16, 80>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
   }
