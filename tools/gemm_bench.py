@@ -102,7 +102,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
     if mode == "w4var":
-        variants(dev, g, 4, [0, 64, 80, 32])
+        variants(dev, g, 4, [0, 128, 4, 8, 136, 12])
     elif mode == "w8var":
         variants(dev, g, 8, [0, 1, 2, 8, 16])
     else:

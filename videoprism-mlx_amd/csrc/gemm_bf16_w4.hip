@@ -34,10 +34,12 @@ constexpr int kThreads = 256;
 constexpr int kOp = BM * BK * 2;             // 32 KiB: one operand's K-tile
 constexpr int kBuf = 2 * kOp;                // A then W
 constexpr int kLds = 2 * kBuf;               // 128 KiB
-// per-wave epilogue scratch: 16 rows x 64 fp32 columns, rows padded by 16 B (bank spread)
-constexpr int kScrRow = 64 * 4 + 16;
-constexpr int kScr = 16 * kScrRow;           // 4352 B
-constexpr int kLdsTotal = kLds + 4 * kScr;   // 148480 B
+// per-wave epilogue scratch: two buffers of 16 rows x 64 fp32 columns (256-B rows), 16-B
+// chunk c of row r stored at chunk c ^ (r & 7) (conflict-free for the ds_write_b128 and
+// ds_read_b128 patterns below, brute-force checked)
+constexpr int kScrBuf = 16 * 256;
+constexpr int kScr = 2 * kScrBuf;            // 8 KiB per wave
+constexpr int kLdsTotal = kLds + 4 * kScr;   // 163840 B = all 160 KiB
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -50,7 +52,8 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // (lets the stores drain behind the next tile; correct, measured no faster), 32 = epilogue
 // without its global stores (LDS transposition and math kept), 64 = start skew: workgroup
 // group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
-// K-tile, so the tiles' epilogue store bursts do not coincide across the chip.
+// K-tile, so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
+// schedule with the 16 loads and 16 reads in its first 32 MFMAs.
 template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -198,18 +201,28 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
 #pragma unroll
     for (int idx = 2; idx < 64; ++idx) mfma(1, idx, false);
+    if constexpr (DIAG & 128) {  // front-loaded: loads and reads within the first 32 MFMAs
 #pragma unroll
-    for (int q = 0; q < 15; ++q) {
+      for (int q = 0; q < 16; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 15; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     sched_fence();
     advance();  // after the scheduled block: its branch must not split it
   };
@@ -220,7 +233,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
   }
+  const int er = lane >> 3, es = lane & 7;  // epilogue read-back: row pass*8 + er, column segment es
   for (int j = 0; j < count; ++j) {
+    // this tile's bias columns, requested before any of the tile's K-stream loads: vmcnt
+    // retires in issue order, so a bias load issued in the epilogue would wait for the next
+    // tile's prefetch
+    float4 bl[2], bh[2];
+    {
+      const int tile = first + j * stride;
+      const int nb = (tile % tilesN) * BN + wn * 128 + es * 8;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+        bl[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64);
+        bh[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64 + 4);
+      }
+    }
     h0(g & 1, true);
     h1(g & 1, (DIAG & 16) && j > 0);
     ++g;
@@ -241,54 +268,54 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const int m0 = (tile / tilesN) * BM + wm * 128, n0 = (tile % tilesN) * BN + wn * 128;
     using Tr = EpiTraits<EPI>;
     char* scr = smem + kLds + w * kScr;
-    const int er = lane >> 3, es = lane & 7;  // read-back: row pass*8 + er, column segment es
-    float4 bl[2], bh[2];
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh) {
-      bl[nh] = *reinterpret_cast<const float4*>(ep.bias + n0 + nh * 64 + es * 8);
-      bh[nh] = *reinterpret_cast<const float4*>(ep.bias + n0 + nh * 64 + es * 8 + 4);
-    }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)
     F8 ex[2][2][2];  // [buffer][nh][pass]
-    auto fetch = [&](int b, int mt) {
+    auto fetch = [&](int bsel, int mt) {
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
         for (int pass = 0; pass < 2; ++pass)
-          ex[b][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+          ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+    };
+    // block G = (mt, nh): acc[nh*4 + q][mt], q = 0..3 -> scratch buffer G & 1.  Block G+1 is
+    // written before block G is read back, so the LDS round trip overlaps the math and stores.
+    auto put = [&](int G) {
+      const int mt = G >> 1, nh = G & 1;
+      char* sb = scr + (G & 1) * kScrBuf + frow * 256;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(sb + (((q * 4 + (lane >> 4)) ^ (frow & 7)) << 4)) = acc[nh * 4 + q][mt];
     };
     if constexpr (Tr::kExtra) fetch(0, 0);
+    put(0);
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+    for (int G = 0; G < 16; ++G) {
+      const int mt = G >> 1, nh = G & 1;
+      if (G + 1 < 16) put(G + 1);
       if constexpr (Tr::kExtra) {
-        if (mt < 7) fetch((mt + 1) & 1, mt + 1);
+        if (nh == 0 && mt < 7) fetch((mt + 1) & 1, mt + 1);
       }
 #pragma unroll
-      for (int nh = 0; nh < 2; ++nh) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *reinterpret_cast<f32x4*>(scr + frow * kScrRow + (q * 16 + (lane >> 4) * 4) * 4) = acc[nh * 4 + q][mt];
-#pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {
-          const int rl = pass * 8 + er;
-          const int row = m0 + mt * 16 + rl;
-          const int n = n0 + nh * 64 + es * 8;
-          F8 v;
-          v.lo = *reinterpret_cast<const float4*>(scr + rl * kScrRow + es * 32);
-          v.hi = *reinterpret_cast<const float4*>(scr + rl * kScrRow + es * 32 + 16);
-          v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
-          v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
-          float keep = 1.0f;
-          if constexpr (Tr::kKeep) {
-            if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
-          }
-          if constexpr (DIAG & 32) {
-            if (ep.ldo == -12345) epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
-            else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
-          } else {
-            epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
-          }
+      for (int pass = 0; pass < 2; ++pass) {
+        const int rl = pass * 8 + er;
+        const int row = m0 + mt * 16 + rl;
+        const int n = n0 + nh * 64 + es * 8;
+        const char* sb = scr + (G & 1) * kScrBuf + rl * 256;
+        F8 v;
+        v.lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
+        v.hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
+        v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
+        v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
+        float keep = 1.0f;
+        if constexpr (Tr::kKeep) {
+          if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
+        }
+        if constexpr (DIAG & 32) {
+          if (ep.ldo == -12345) epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
+        } else {
+          epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
         }
       }
     }
@@ -344,6 +371,9 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 32: return launch_w4<EPI_BF16, 32>(A, lda, W, ldw, M, N, K, ep, s);
       case 64: return launch_w4<EPI_BF16, 64>(A, lda, W, ldw, M, N, K, ep, s);
       case 80: return launch_w4<EPI_BF16, 80>(A, lda, W, ldw, M, N, K, ep, s);
+      case 12: return launch_w4<EPI_BF16, 12>(A, lda, W, ldw, M, N, K, ep, s);
+      case 128: return launch_w4<EPI_BF16, 128>(A, lda, W, ldw, M, N, K, ep, s);
+      case 136: return launch_w4<EPI_BF16, 136>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
   }
