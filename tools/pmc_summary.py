@@ -44,3 +44,34 @@ for k, cs in vals.items():
         print(f"   => HBM read ~ {2*m['FETCH_SIZE']*1024/1e6:.1f} MB (FETCH_SIZE x2, gfx950 rule)")
     if "WRITE_SIZE" in m:
         print(f"   => HBM write ~ {m['WRITE_SIZE']*1024/1e6:.1f} MB")
+
+
+# --json OUT: per-launch HBM bytes of the bench's kernel classes (bench.py reads it for the
+# roofline's `traffic`): 2 x FETCH_SIZE (gfx950 rule) + WRITE_SIZE, KiB counters.
+CLASS_OF = {  # kernel instance -> vp_profile class (vp_abi.cpp kProfNames)
+    "gemm_bf16_w4_kernel<1, 0>": "gemm_ffn1_gelu",
+    "gemm_bf16_w4_kernel<7, 0>": "gemm_ffn2",
+    "gemm_bf16_w4_kernel<0, 0>": "gemm_qkv",
+    "gemm_bf16_w4_kernel<5, 0>": "gemm_post",
+    "gemm_bf16_w4_kernel<6, 0>": "gemm_patch_embed",
+    "attn_spatial_kernel<false>": "attention_spatial",
+    "attn_temporal_kernel<false>": "attention_temporal",
+}
+if len(sys.argv) > 3 and sys.argv[2] == "--json":
+    import json
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes ({root}); "
+                     "hbm_bytes_per_launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md "
+                     "HBM section: FETCH_SIZE reads half of wide streaming reads on gfx950; Infinity-Cache "
+                     "hits are counted)", "kernels": {}}
+    for k, cs in vals.items():
+        cls = CLASS_OF.get(k)
+        if not cls or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
+        w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
+        out["kernels"][cls] = {"kernel": k, "fetch_bytes": 2 * f * 1024, "write_bytes": w * 1024,
+                               "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+                               "dispatches": len(cs["FETCH_SIZE"])}
+    with open(sys.argv[3], "w") as fo:
+        json.dump(out, fo, indent=1)
+    print("wrote", sys.argv[3])
