@@ -60,15 +60,22 @@ def compare(dev, g):
         same = bool(torch.equal(outs[4], outs[8]))
         del outs
         o = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        f8 = lambda: nat.dev_gemm_kernel(8, a, w, b, epi, o, resid=o if resid else None)
-        f4 = lambda: nat.dev_gemm_kernel(4, a, w, b, epi, o, resid=o if resid else None)
-        res = {"w8": [], "w4": [], "torch": []}
+        o2 = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        nat.dev_gemm_kernel(2, a, w, b, epi, o2, resid=o2 if resid else None)
+        o4 = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        nat.dev_gemm_kernel(4, a, w, b, epi, o4, resid=o4 if resid else None)
+        same_ov = bool(torch.equal(o2, o4))
+        del o2, o4
+        fns = {"w8": lambda: nat.dev_gemm_kernel(8, a, w, b, epi, o, resid=o if resid else None),
+               "w4": lambda: nat.dev_gemm_kernel(4, a, w, b, epi, o, resid=o if resid else None),
+               "ov": lambda: nat.dev_gemm_kernel(2, a, w, b, epi, o, resid=o if resid else None),
+               "torch": lambda: torch.matmul(a, w.t())}
+        res = {k: [] for k in fns}
         for _ in range(3):  # interleaved rounds
-            res["w8"].append(timeit(f8))
-            res["w4"].append(timeit(f4))
-            res["torch"].append(timeit(lambda: torch.matmul(a, w.t())))
+            for k, f in fns.items():
+                res[k].append(timeit(f))
         flop = 2.0 * M * N * K
-        print(f"{name:5s} M={M} N={N} K={K} epi={epi} w4==w8:{same}: " + " | ".join(
+        print(f"{name:5s} M={M} N={N} K={K} epi={epi} w4==w8:{same} ov==w4:{same_ov}: " + " | ".join(
             f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
 
 
@@ -80,8 +87,8 @@ def variants(dev, g, which, diags):
         res = {d: [] for d in diags}
         for _ in range(3):
             for d in diags:
-                if which == 4:
-                    f = lambda: nat.dev_gemm_kernel(4, a, w, b, (1000 + d) if d else 0, o)
+                if which in (2, 4):
+                    f = lambda: nat.dev_gemm_kernel(which, a, w, b, (1000 + d) if d else 0, o)
                 else:
                     lib = nat.load()
                     fn = lib.vp_dev_gemm_diag
@@ -101,7 +108,14 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    if mode == "w4var":
+    if mode == "nt":
+        variants(dev, g, 4, [0, 256, 8])
+    elif mode == "cmp":
+        compare(dev, g)
+        variants(dev, g, 2, [0, 1, 8, 16])
+    elif mode == "ovvar":
+        variants(dev, g, 2, [0, 1, 8, 16])
+    elif mode == "w4var":
         variants(dev, g, 4, [0, 128, 4, 8, 136, 12])
     elif mode == "w8var":
         variants(dev, g, 8, [0, 1, 2, 8, 16])

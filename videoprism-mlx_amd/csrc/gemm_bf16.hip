@@ -406,13 +406,15 @@ hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W
   static int mode = -1;
   if (mode < 0) {
     const char* e = getenv("VP_GEMM_KERNEL");
-    mode = (e && !strcmp(e, "w8")) ? 8 : (e && !strcmp(e, "w4")) ? 4 : 0;
+    mode = (e && !strcmp(e, "w8")) ? 8 : (e && !strcmp(e, "w4")) ? 4 : (e && !strcmp(e, "ov")) ? 2 : 0;
   }
+  if (mode == 2 && gemm_bf16_ov_ok(epi, M, N, K, lda, ldw))
+    return gemm_bf16_ov(epi, A, lda, W, ldw, M, N, K, ep, s);
   const bool w4_ok = (uint64_t)M * (uint64_t)lda * 2 < 0xFFFFFFF0ull &&
                      (uint64_t)N * (uint64_t)ldw * 2 < 0xFFFFFFF0ull;
   bool use_w4 = w4_ok;
   if (mode == 8) use_w4 = false;
-  else if (mode == 0 && (epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024) use_w4 = false;
+  else if (mode != 4 && (epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024) use_w4 = false;
   if (use_w4) return gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s);
   return gemm_bf16(epi, A, lda, W, ldw, M, N, K, ep, s);
 }

@@ -1,0 +1,592 @@
+// bf16 GEMM whose epilogue runs UNDER the next tile's MFMAs ("ov"), persistent, 4 waves.
+//
+//   C[M,N] = A[M,K] . W[N,K]^T  (+ fused epilogue, bf16 out), 256x128 tile, BK = 64.
+//
+// Why (tools/gemm_bench.py): the 256x256 one-accumulator-set kernel
+// (gemm_bf16_w4.hip) spends ~1/3 of its time in the epilogue with the MFMA pipe idle -- a
+// CU's stores issue at ~14 B/cycle, so a 128 KiB output tile costs ~9k cycles however the
+// tiles are skewed, and a wave cannot start the next tile while it still owns the 256
+// accumulators.  Here a wave owns 128x64 outputs = 128 fp32 accumulators and keeps TWO sets
+// (256 AGPRs): tile j computes into one set while tile j-1's set is drained, one 16-row
+// group per K-tile, by instructions interleaved with tile j's MFMAs:
+//     K-tile slot G+2, h0:  4 ds_write_b128 of group G into the wave's LDS scratch
+//     K-tile slot G+2, h1:  read back (a lane owns 8 consecutive columns of one row), bias /
+//                           GELU / residual / pos math in fp32, 2 full-line stores
+//     K-tile slot G,   h1:  residual / pos / pad rows of group G requested (inline-asm loads,
+//                           retired by the counted vmcnt two K-tiles later)
+// Only the last tile of each workgroup has an exposed epilogue.
+//
+// Pipeline: 3 LDS stages of 48 KiB (A 256x64, W 128x64, 128-byte rows, swizzle chunk ^=
+// (row>>1)&7 applied on the DMA source and undone on the ds_read_b128), staged by
+// buffer_load_dwordx4 ... lds in pieces of 8 rows x 128 B (12 per wave per K-tile).  K-tile g
+// = two k-halves: h0 MFMAs on fragment set 0 while set 1 is read; h1 waits (counted vmcnt),
+// one barrier, MFMAs on set 1 while set 0 of K-tile g+1 is read and K-tile g+3 is loaded
+// into the buffer K-tile g just released.  Every h1 waits vmcnt(#vector-memory ops issued by
+// the previous h1), i.e. exactly for the operations older than them: K-tile g+1's pieces,
+// and the epilogue loads/stores issued two K-tiles earlier.
+// 16x16x32 MFMA (the chip holds a higher clock on it than on 32x32x16 under load), W as the
+// A operand so a lane's accumulators are 4 consecutive output columns of one row.
+#include <type_traits>
+
+#include "gemm_epilogue.h"
+
+namespace vp {
+
+namespace {
+
+constexpr int BM = 256, BN = 128, BK = 64;
+constexpr int kThreads = 256;
+constexpr int kOpA = BM * BK * 2;            // 32 KiB
+constexpr int kOpW = BN * BK * 2;            // 16 KiB
+constexpr int kBuf = kOpA + kOpW;            // one stage
+constexpr int kStages = 3;
+constexpr int kLds = kStages * kBuf;         // 144 KiB
+constexpr int kScr = 16 * 256;               // per-wave scratch: 16 rows x 64 fp32, 256-B rows
+constexpr int kLdsTotal = kLds + 4 * kScr;   // 163840 B = all 160 KiB
+constexpr int kPieces = 12;                  // LDS-DMA pieces per wave per K-tile
+constexpr int kGroups = 8;                   // 16-row groups of a wave's 128x64 outputs
+constexpr int kLag = 2;                      // group G is put/read back in K-tile slot G + kLag
+constexpr int kSlots = kGroups + kLag + 1;   // slots 0..10 unrolled (stores of group G: slot
+                                             // G + 3); K-tile >= 11 plain
+constexpr int kMinK = kSlots * BK;           // K >= 704
+
+#define VP_AI __attribute__((always_inline))
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+
+template <int S, int N, class F>
+__device__ __forceinline__ void static_for(F& f) {
+  if constexpr (S < N) {
+    f(std::integral_constant<int, S>{});
+    static_for<S + 1, N>(f);
+  }
+}
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// Loads the compiler does not see: they are retired by the pipeline's counted vmcnt (a
+// compiler-visible load would make hipcc wait vmcnt(0) at its first use and drain the DMA
+// stream).  `launder` after the retiring wait keeps every use behind that wait.
+__device__ __forceinline__ u32x4 gld16(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+__device__ __forceinline__ float gld4(const void* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+  return v;
+}
+// SGPR base + VGPR 32-bit offset (saddr form)
+__device__ __forceinline__ u32x4 gld16s(const char* sbase, uint32_t voff) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase));
+  return v;
+}
+__device__ __forceinline__ float gld4s(const char* sbase, uint32_t voff) {
+  float v;
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase));
+  return v;
+}
+template <class T>
+__device__ __forceinline__ void launder(T& x) {
+  asm volatile("" : "+v"(x));
+}
+// LDS read the compiler does not see (a visible read of the scratch gets a vmcnt wait for the
+// in-flight LDS-DMA pieces inserted in front of it); retired by the next lgkmcnt(0)
+__device__ __forceinline__ float4 lds_rd16(uint32_t addr) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int EPI, bool PAD>
+struct OvEpi {
+  using Tr = EpiTraits<EPI>;
+  static_assert(Tr::kOutBf16 && !Tr::kResidF32, "ov kernel: bf16-output epilogues only");
+  static constexpr bool kResid = Tr::kResidBf16;
+  static constexpr bool kPos = Tr::kPos;
+  static constexpr bool kPad = PAD && Tr::kKeep;
+  // epilogue loads per group (2 passes of 8 rows)
+  static constexpr int kLoads = 2 * ((kResid ? 1 : 0) + (kPos ? 2 : 0) + (kPad ? 1 : 0));
+};
+
+// Vector-memory operations of K-tile slot s (EP: a tile is being drained): the h1 issues the
+// drained tile's bias (slot 0) and group-s operand loads (slots 0..7) before its 12 DMA pieces;
+// the h0 issues group s-3's 2 stores (slots 3..10).  Slots < 0 or >= kSlots are plain.
+template <int EPI, bool PAD, bool EP>
+constexpr int vm_h1(int s) {
+  if (!EP || s < 0 || s >= kSlots) return kPieces;
+  return kPieces + (s == 0 ? 2 : 0) + (s < kGroups ? OvEpi<EPI, PAD>::kLoads : 0);
+}
+template <int EPI, bool PAD, bool EP>
+constexpr int vm_h0(int s) {
+  return (EP && s >= kLag + 1 && s < kGroups + kLag + 1) ? 2 : 0;
+}
+// The h1 of slot s reads K-tile s+1, whose pieces the h1 of slot s-2 issued; every operation
+// issued after those may stay in flight.  (An under-count only over-waits, so slot 0 and the
+// plain slots use the pieces-only count.)
+template <int EPI, bool PAD, bool EP>
+constexpr int vm_wait(int s) {
+  if (s <= 0 || s >= kSlots) return kPieces;
+  return vm_h0<EPI, PAD, EP>(s - 1) + vm_h1<EPI, PAD, EP>(s - 1) + vm_h0<EPI, PAD, EP>(s);
+}
+
+struct GroupX {  // one group's epilogue operands (only the fields an epilogue uses survive)
+  u32x4 r[2];     // bf16 residual rows, pass 0/1
+  u32x4 p[2][2];  // fp32 position rows, pass 0/1, lo/hi
+  float pad[2];   // row padding
+};
+
+// DIAG (ablation builds for tools/gemm_bench.py; results garbage): 1 = no epilogue (tiles'
+// accumulators kept live by a never-taken branch), 2 = no fragment ds_reads in the K loop,
+// 4 = no DMA pieces after the prologue, 8 = epilogue without its global stores, 16 = epilogue
+// without the LDS put / read-back
+template <int EPI, bool PAD, int DIAG = 0>
+__global__ __launch_bounds__(kThreads, 1) void gemm_bf16_ov_kernel(
+    const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
+    int N, int K, EpiArgs ep) {
+  using E = OvEpi<EPI, PAD>;
+  using Tr = EpiTraits<EPI>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tilesN = N / BN;
+  const int T = (M / BM) * tilesN;
+  const int G = gridDim.x;
+  const int b = blockIdx.x;
+  int first, stride, count;
+  if ((G & 7) == 0) {  // XCD x owns tiles [x*T/8, (x+1)*T/8), tn fastest
+    const int xcd = b & 7, li = b >> 3, nx = G >> 3;
+    const int lo = (int)(((int64_t)xcd * T) >> 3), hi = (int)(((int64_t)(xcd + 1) * T) >> 3);
+    first = lo + li;
+    stride = nx;
+    count = first < hi ? (hi - first + nx - 1) / nx : 0;
+  } else {
+    first = b;
+    stride = G;
+    count = b < T ? (T - b + G - 1) / G : 0;
+  }
+  if (count == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int w = wave_id();
+  const int wm = w >> 1, wn = w & 1;
+  const int nk = K / BK;
+  const int total = count * nk;
+
+  // ---- staging: wave w fills A pieces w*8+i (i < 8) and W pieces w*4+i (i < 4)
+  const uint32_t a_rb = (uint32_t)(lda * 2), w_rb = (uint32_t)(ldw * 2);
+  const uint64_t a_bytes = (uint64_t)M * a_rb, w_bytes = (uint64_t)N * w_rb;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)(uint32_t)a_bytes, 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, (int)(uint32_t)w_bytes, 0x00020000);
+  const int prow = lane >> 3;
+  const uint32_t cE = (uint32_t)((lane & 7) ^ swz(prow)) * 16;
+  const uint32_t cO = (uint32_t)((lane & 7) ^ swz(prow + 8)) * 16;
+  const uint32_t vA[2] = {prow * a_rb + cE, prow * a_rb + cO};
+  const uint32_t vW[2] = {prow * w_rb + cE, prow * w_rb + cO};
+  typedef __attribute__((address_space(3))) void lds_void;
+  int ld_g = 0, ld_kt = 0, ld_tile = first, ld_buf = 0;
+  int ld_tm = ld_tile / tilesN, ld_tn = ld_tile - ld_tm * tilesN;
+  auto advance = [&]() VP_AI {  // the tail re-loads the last K-tile into a free buffer (harmless)
+    ld_buf = ld_buf == kStages - 1 ? 0 : ld_buf + 1;
+    if (ld_g + 1 >= total) return;
+    ++ld_g;
+    if (++ld_kt == nk) {
+      ld_kt = 0;
+      ld_tile += stride;
+      ld_tm = ld_tile / tilesN;
+      ld_tn = ld_tile - ld_tm * tilesN;
+    }
+  };
+  auto stage_piece = [&](int p) VP_AI {  // p < 8: A piece, else W piece; into buffer ld_buf
+    char* base = smem + ld_buf * kBuf;
+    if (p < 8) {
+      const uint32_t so = (uint32_t)(ld_tm * BM + (w * 8 + p) * 8) * a_rb + ld_kt * (BK * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)(base + (w * 8 + p) * 1024), 16,
+                                               vA[p & 1], so, 0, 0);
+    } else {
+      const int i = p - 8;
+      const uint32_t so = (uint32_t)(ld_tn * BN + (w * 4 + i) * 8) * w_rb + ld_kt * (BK * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void*)(base + kOpA + (w * 4 + i) * 1024), 16,
+                                               vW[i & 1], so, 0, 0);
+    }
+  };
+
+  // ---- fragments (16x16x32): rows (lane&15), 16-byte chunk kh*4 + (lane>>4)
+  const int frow = lane & 15;
+  int aoff[2], woff[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const int ch = ((kh * 4 + (lane >> 4)) ^ swz(frow)) * 16;
+    aoff[kh] = (wm * 128 + frow) * 128 + ch;
+    woff[kh] = kOpA + (wn * 64 + frow) * 128 + ch;
+  }
+  bf16x8 fa[2][8], fw[2][4];
+  auto rd = [&](int set, int buf, int q) VP_AI {
+    if constexpr (DIAG & 2) {
+      if (q < 8) asm volatile("" : "+v"(fa[set][q]));
+      else asm volatile("" : "+v"(fw[set][q - 8]));
+      return;
+    }
+    const char* base = smem + buf * kBuf;
+    if (q < 8) fa[set][q] = *reinterpret_cast<const bf16x8*>(base + aoff[set] + q * 2048);
+    else fw[set][q - 8] = *reinterpret_cast<const bf16x8*>(base + woff[set] + (q - 8) * 2048);
+  };
+
+  f32x4 accX[4][8], accY[4][8];
+  auto mfma = [&](auto C, int set, int idx, bool zero) VP_AI {  // idx = nt*8 + mt
+    const int nt = idx >> 3, mt = idx & 7;
+    if constexpr (decltype(C)::value == 0)
+      accX[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[set][nt], fa[set][mt],
+                                                             zero ? f32x4{0.f, 0.f, 0.f, 0.f} : accX[nt][mt], 0, 0, 0);
+    else
+      accY[nt][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[set][nt], fa[set][mt],
+                                                             zero ? f32x4{0.f, 0.f, 0.f, 0.f} : accY[nt][mt], 0, 0, 0);
+  };
+
+  // ---- epilogue state of the tile being drained
+  char* scr = smem + kLds + w * kScr;
+  const int er = lane >> 3, es = lane & 7;
+  float4 bl, bh;     // bias columns es*8 .. +7 of the drained tile's wave columns
+  GroupX gx[3];      // group G's operands live in gx[G % 3] from slot G to slot G + 2
+  int e_m0 = 0, e_n0 = 0;  // drained tile: first row / column of this wave
+  // epilogue addresses: a wave-uniform (SGPR) row base + a 32-bit per-lane offset
+  auto load_bias = [&]() VP_AI {
+    const char* sb = reinterpret_cast<const char*>(ep.bias + e_n0);
+    const u32x4 a = gld16s(sb, es * 32), c = gld16s(sb, es * 32 + 16);
+    bl = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(a.z), __uint_as_float(a.w));
+    bh = make_float4(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z), __uint_as_float(c.w));
+  };
+  auto launder_bias = [&]() VP_AI {
+    launder(bl.x); launder(bl.y); launder(bl.z); launder(bl.w);
+    launder(bh.x); launder(bh.y); launder(bh.z); launder(bh.w);
+  };
+  auto load_group = [&](GroupX& x, int g) VP_AI {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int r0 = e_m0 + g * 16 + pass * 8;  // wave-uniform
+      if constexpr (E::kResid) {
+        const char* sb = reinterpret_cast<const char*>(static_cast<const bf16_t*>(ep.resid) +
+                                                       (int64_t)r0 * ep.ldr + e_n0);
+        x.r[pass] = gld16s(sb, (uint32_t)(er * ep.ldr + es * 8) * 2);
+      }
+      if constexpr (E::kPos) {
+        const float* pp = ep.pos + (int64_t)((r0 + er) % ep.pos_rows) * N + e_n0 + es * 8;
+        x.p[pass][0] = gld16(pp);
+        x.p[pass][1] = gld16(pp + 4);
+      }
+      if constexpr (E::kPad) x.pad[pass] = gld4s(reinterpret_cast<const char*>(ep.rowpad + r0), er * 4);
+    }
+  };
+  auto launder_group = [&](GroupX& x) VP_AI {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if constexpr (E::kResid) launder(x.r[pass]);
+      if constexpr (E::kPos) { launder(x.p[pass][0]); launder(x.p[pass][1]); }
+      if constexpr (E::kPad) launder(x.pad[pass]);
+    }
+  };
+  // group g of set S -> scratch (lane: row frow, 16-B chunk (nt*4 + lane>>4) ^ (frow & 7))
+  auto put = [&](auto S, int g) VP_AI {
+    if constexpr (DIAG & 16) return;
+    char* sb = scr + frow * 256;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      f32x4 v;
+      if constexpr (decltype(S)::value == 0) v = accX[nt][g]; else v = accY[nt][g];
+      *reinterpret_cast<f32x4*>(sb + (((nt * 4 + (lane >> 4)) ^ (frow & 7)) << 4)) = v;
+    }
+  };
+  F8 rb[2];  // read-back values of the group being finished
+  const uint32_t scr_lds = (uint32_t)(uintptr_t)VP_LDS_PTR(scr);
+  auto readback = [&]() VP_AI {
+    if constexpr (DIAG & 16) return;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int rl = pass * 8 + er;
+      const uint32_t sb = scr_lds + rl * 256;
+      rb[pass].lo = lds_rd16(sb + (((2 * es) ^ (rl & 7)) << 4));
+      rb[pass].hi = lds_rd16(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
+    }
+  };
+  auto launder_rb = [&]() VP_AI {
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      launder(rb[pass].lo.x); launder(rb[pass].lo.y); launder(rb[pass].lo.z); launder(rb[pass].lo.w);
+      launder(rb[pass].hi.x); launder(rb[pass].hi.y); launder(rb[pass].hi.z); launder(rb[pass].hi.w);
+    }
+  };
+  auto finish = [&](const GroupX& x, int g) VP_AI {  // math + 2 full-line stores of group g
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      F8 v = rb[pass];
+      v.lo.x += bl.x; v.lo.y += bl.y; v.lo.z += bl.z; v.lo.w += bl.w;
+      v.hi.x += bh.x; v.hi.y += bh.y; v.hi.z += bh.z; v.hi.w += bh.w;
+      float keep = 1.0f;
+      if constexpr (E::kPad) keep = 1.0f - x.pad[pass];
+      F8 ex;
+      if constexpr (E::kResid) {
+        ex.lo = bf16x4_to_f32(make_uint2(x.r[pass].x, x.r[pass].y));
+        ex.hi = bf16x4_to_f32(make_uint2(x.r[pass].z, x.r[pass].w));
+      } else if constexpr (E::kPos) {
+        ex.lo = *reinterpret_cast<const float4*>(&x.p[pass][0]);
+        ex.hi = *reinterpret_cast<const float4*>(&x.p[pass][1]);
+      } else {
+        ex.lo = ex.hi = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      v.lo = epi_math4(v.lo, keep, ex.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra);
+      v.hi = epi_math4(v.hi, keep, ex.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra);
+      const int r0 = e_m0 + g * 16 + pass * 8;  // wave-uniform
+      char* sb = reinterpret_cast<char*>(static_cast<bf16_t*>(ep.out) + (int64_t)r0 * ep.ldo + e_n0);
+      const uint4 pk = make_uint4(pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w),
+                                  pack_bf16x2(v.hi.x, v.hi.y), pack_bf16x2(v.hi.z, v.hi.w));
+      if constexpr (DIAG & 8) {
+        asm volatile("" ::"v"(pk.x), "v"(pk.y), "v"(pk.z), "v"(pk.w));
+      } else {
+        __builtin_nontemporal_store(u32x4{pk.x, pk.y, pk.z, pk.w},
+                                    reinterpret_cast<u32x4*>(sb + (uint32_t)(er * ep.ldo + es * 8) * 2));
+      }
+    }
+  };
+
+  // ---- prologue: K-tiles 0, 1, 2 into buffers 0, 1, 2; fragments of (0, h0)
+#pragma unroll
+  for (int st = 0; st < kStages; ++st) {
+#pragma unroll
+    for (int p = 0; p < kPieces; ++p) stage_piece(p);
+    advance();
+  }
+  wait_vm<2 * kPieces>();
+  sched_fence();
+  __builtin_amdgcn_s_barrier();
+  sched_fence();
+#pragma unroll
+  for (int q = 0; q < 12; ++q) rd(0, 0, q);
+
+  // h0 of K-tile slot s (buffer cb): MFMAs on set 0 while set 1 <- (g, h1) is read; with a
+  // drained tile: puts group PG into the scratch and finishes group FG (math + 2 stores)
+  auto h0 = [&](auto C, int cb, bool zero, auto PG, auto FG) VP_AI {
+    constexpr int pg = decltype(PG)::value, fg = decltype(FG)::value;
+    constexpr int D = 1 - decltype(C)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (fg >= 0) {
+      launder_rb();
+      if constexpr (fg == 0) launder_bias();
+      if constexpr (E::kLoads > 0) launder_group(gx[fg % 3]);
+    }
+    sched_fence();
+#pragma unroll
+    for (int q = 0; q < 12; ++q) rd(1, cb, q);
+#pragma unroll
+    for (int idx = 0; idx < 32; ++idx) mfma(C, 0, idx, zero);
+    if constexpr (pg >= 0) put(std::integral_constant<int, D>{}, pg);
+    if constexpr (fg >= 0) finish(gx[fg % 3], fg);
+    if constexpr (pg >= 0 || fg >= 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        if (r == 7 || r == 15) __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 12; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    }
+    sched_fence();
+  };
+
+  // h1 of K-tile slot s (buffer cb; next K-tile in nb): counted vmcnt, barrier, MFMAs on set 1
+  // while set 0 <- (g+1, h0) is read and K-tile g+3 is loaded into buffer cb.  With a drained
+  // tile: reads back group s-kLag (put by this slot's h0) and requests the bias (slot 0) and
+  // group s's operands, all before the pieces.  s < 0: plain K-tile.
+  auto h1 = [&](auto C, int cb, int nb, auto SL, auto CNT, auto EP) VP_AI {
+    constexpr int s = decltype(SL)::value;
+    constexpr bool ep_on = decltype(EP)::value && s >= 0;
+    constexpr bool do_bias = ep_on && s == 0;
+    constexpr bool do_load = ep_on && s < kGroups && E::kLoads > 0;
+    constexpr bool do_rb = ep_on && s >= kLag && s < kGroups + kLag;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vm<decltype(CNT)::value>();
+    sched_fence();
+    mfma(C, 1, 0, false);
+    mfma(C, 1, 1, false);
+    sched_fence();
+    __builtin_amdgcn_s_barrier();
+    sched_fence();
+    if constexpr (do_rb) readback();
+    if constexpr (do_bias) load_bias();
+    if constexpr (do_load) load_group(gx[s % 3], s);
+    sched_fence();
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      rd(0, nb, q);
+      if constexpr (!(DIAG & 4)) stage_piece(q);
+    }
+#pragma unroll
+    for (int idx = 2; idx < 32; ++idx) mfma(C, 1, idx, false);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    sched_fence();
+    advance();
+  };
+
+  // one tile computed into set C; the previous tile (set 1-C) drained when EP
+  int g = 0;  // global K-tile counter (buffer = g % 3)
+  auto body = [&](auto C, auto EP, int tile) VP_AI {
+    constexpr bool epv = decltype(EP)::value;
+    auto slot = [&](auto SL) VP_AI {
+      constexpr int s = decltype(SL)::value;
+      const int cb = g % 3, nb = (g + 1) % 3;
+      constexpr int pg = (epv && s >= kLag && s < kGroups + kLag) ? s - kLag : -1;
+      constexpr int fg = (epv && s >= kLag + 1 && s < kGroups + kLag + 1) ? s - kLag - 1 : -1;
+      h0(C, cb, s == 0, std::integral_constant<int, pg>{}, std::integral_constant<int, fg>{});
+      h1(C, cb, nb, SL, std::integral_constant<int, vm_wait<EPI, PAD, epv>(s)>{}, EP);
+      ++g;
+    };
+    static_for<0, kSlots>(slot);
+    for (int kt = kSlots; kt < nk; ++kt, ++g) {
+      const int cb = g % 3, nb = (g + 1) % 3;
+      h0(C, cb, false, std::integral_constant<int, -1>{}, std::integral_constant<int, -1>{});
+      h1(C, cb, nb, std::integral_constant<int, -1>{}, std::integral_constant<int, kPieces>{},
+         std::false_type{});
+    }
+    // this tile becomes the drained one
+    const int tm = tile / tilesN, tn = tile - tm * tilesN;
+    e_m0 = tm * BM + wm * 128;
+    e_n0 = tn * BN + wn * 64;
+  };
+
+  // exposed epilogue of the last tile (set S)
+  auto final_epi = [&](auto S) VP_AI {
+    wait_vm<0>();
+    load_bias();
+    wait_vm<0>();
+    launder_bias();
+#pragma unroll
+    for (int gi = 0; gi < kGroups; ++gi) {
+      load_group(gx[0], gi);
+      put(S, gi);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      sched_fence();
+      readback();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_vm<0>();
+      launder_rb();
+      launder_group(gx[0]);
+      sched_fence();
+      finish(gx[0], gi);
+    }
+  };
+
+  if constexpr (DIAG & 1) {
+    for (int j = 0; j < count; ++j) {
+      body(std::integral_constant<int, 0>{}, std::false_type{}, first + j * stride);
+      if (ep.ldo == -12345) {  // never at run time: keeps every tile's MFMAs live
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int mt = 0; mt < 8; ++mt) asm volatile("" ::"a"(accX[nt][mt]));
+      }
+    }
+  } else {
+    body(std::integral_constant<int, 0>{}, std::false_type{}, first);
+    int j = 1;
+    for (; j + 1 < count; j += 2) {
+      body(std::integral_constant<int, 1>{}, std::true_type{}, first + j * stride);
+      body(std::integral_constant<int, 0>{}, std::true_type{}, first + (j + 1) * stride);
+    }
+    if (j < count) {
+      body(std::integral_constant<int, 1>{}, std::true_type{}, first + j * stride);
+      final_epi(std::integral_constant<int, 1>{});
+    } else {
+      final_epi(std::integral_constant<int, 0>{});
+    }
+  }
+  // drain the tail's (clamped) loads before the workgroup's LDS is released
+  wait_vm<0>();
+}
+
+template <int EPI, bool PAD, int DIAG = 0>
+hipError_t launch_ov(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
+                     int K, const EpiArgs& ep, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_ov_kernel<EPI, PAD, DIAG>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int tiles = (M / BM) * (N / BN);
+  const int grid = tiles < cus ? tiles : cus;
+  hipLaunchKernelGGL((gemm_bf16_ov_kernel<EPI, PAD, DIAG>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda,
+                     W, ldw, M, N, K, ep);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_ov_pad(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
+                         int K, const EpiArgs& ep, hipStream_t s) {
+  if constexpr (EpiTraits<EPI>::kKeep) {
+    if (ep.rowpad) return launch_ov<EPI, true>(A, lda, W, ldw, M, N, K, ep, s);
+  }
+  return launch_ov<EPI, false>(A, lda, W, ldw, M, N, K, ep, s);
+}
+
+}  // namespace
+
+bool gemm_bf16_ov_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw) {
+  if (M % BM || N % BN || K % BK || K < kMinK) return false;
+  if ((uint64_t)M * (uint64_t)lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * (uint64_t)ldw * 2 >= 0xFFFFFFF0ull)
+    return false;
+  return epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RESID_BF16 || epi == EPI_POS_BF16 ||
+         epi == EPI_RESID_FFN_BF16;
+}
+
+hipError_t gemm_bf16_ov(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                        int N, int K, const EpiArgs& ep, hipStream_t s) {
+  if (epi >= 1000) {  // ablation builds, EPI_BF16 epilogue
+    if (!gemm_bf16_ov_ok(EPI_BF16, M, N, K, lda, ldw)) return hipErrorInvalidValue;
+    switch (epi - 1000) {
+      case 1: return launch_ov<EPI_BF16, false, 1>(A, lda, W, ldw, M, N, K, ep, s);
+      case 5: return launch_ov<EPI_BF16, false, 5>(A, lda, W, ldw, M, N, K, ep, s);
+      case 7: return launch_ov<EPI_BF16, false, 7>(A, lda, W, ldw, M, N, K, ep, s);
+      case 8: return launch_ov<EPI_BF16, false, 8>(A, lda, W, ldw, M, N, K, ep, s);
+      case 16: return launch_ov<EPI_BF16, false, 16>(A, lda, W, ldw, M, N, K, ep, s);
+    }
+    return hipErrorInvalidValue;
+  }
+  if (!gemm_bf16_ov_ok(epi, M, N, K, lda, ldw)) return hipErrorInvalidValue;
+  switch (epi) {
+    case EPI_BF16: return launch_ov_pad<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_GELU_BF16: return launch_ov_pad<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16: return launch_ov_pad<EPI_RESID_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_BF16: return launch_ov_pad<EPI_POS_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16: return launch_ov_pad<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace vp

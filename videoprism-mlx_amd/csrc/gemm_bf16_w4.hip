@@ -23,6 +23,8 @@
 //    one M row (8-byte bf16 / 16-byte fp32 stores), as in gemm_bf16.hip.
 //  * The K-tile stream runs across the persistent workgroup's tiles: the next tile's first
 //    K-tiles load during this tile's last K-tiles and epilogue.
+#include <cstdlib>
+
 #include "gemm_epilogue.h"
 
 namespace vp {
@@ -53,7 +55,7 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // without its global stores (LDS transposition and math kept), 64 = start skew: workgroup
 // group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
 // K-tile, so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
-// schedule with the 16 loads and 16 reads in its first 32 MFMAs.
+// schedule with the 16 loads and 16 reads in its first 32 MFMAs, 256 = plain (temporal) output stores.
 template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           if (ep.ldo == -12345) epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
           else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
         } else {
-          epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          epi_store8<EPI, !(DIAG & 256)>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
         }
       }
     }
@@ -374,8 +376,23 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 12: return launch_w4<EPI_BF16, 12>(A, lda, W, ldw, M, N, K, ep, s);
       case 128: return launch_w4<EPI_BF16, 128>(A, lda, W, ldw, M, N, K, ep, s);
       case 136: return launch_w4<EPI_BF16, 136>(A, lda, W, ldw, M, N, K, ep, s);
+      case 256: return launch_w4<EPI_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
+  }
+  static int nt = -1;
+  if (nt < 0) {
+    const char* e = getenv("VP_GEMM_NT");
+    nt = (e && e[0] == '0') ? 0 : 1;
+  }
+  if (!nt) {  // plain (temporal) output stores
+    switch (epi) {
+      case EPI_BF16: return launch_w4<EPI_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+      case EPI_GELU_BF16: return launch_w4<EPI_GELU_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+      case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+      case EPI_POS_BF16: return launch_w4<EPI_POS_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+      case EPI_RESID_FFN_BF16: return launch_w4<EPI_RESID_FFN_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+    }
   }
   switch (epi) {
     case EPI_BF16: return launch_w4<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s);

@@ -140,19 +140,32 @@ __device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, 
 }
 
 // v = acc + bias (8 columns); same math and single rounding as epi_store
-template <int EPI>
+typedef unsigned epi_u32x4 __attribute__((ext_vector_type(4)));
+// NT: nontemporal output stores (global_store ... nt).  Measured on the w4 kernel at the
+// encoder's shapes: qkv 432 -> 379 us, post 147 -> 130 us, ffn1 579 -> 502 us (the output
+// streams past L2 instead of being written back from it later; tools/gemm_bench.py nt).
+template <int EPI, bool NT = true>
 __device__ __forceinline__ void epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
   using Tr = EpiTraits<EPI>;
   v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra);
   v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra);
   if constexpr (Tr::kOutBf16) {
-    *reinterpret_cast<uint4*>(static_cast<bf16_t*>(ep.out) + (int64_t)row * ep.ldo + n) =
-        make_uint4(pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
-                   pack_bf16x2(v.hi.z, v.hi.w));
+    const epi_u32x4 pk = {pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
+                          pack_bf16x2(v.hi.z, v.hi.w)};
+    epi_u32x4* dst = reinterpret_cast<epi_u32x4*>(static_cast<bf16_t*>(ep.out) + (int64_t)row * ep.ldo + n);
+    if constexpr (NT) __builtin_nontemporal_store(pk, dst);
+    else *dst = pk;
   } else {
-    float* o = static_cast<float*>(ep.out) + (int64_t)row * ep.ldo + n;
-    *reinterpret_cast<float4*>(o) = v.lo;
-    *reinterpret_cast<float4*>(o + 4) = v.hi;
+    typedef float f4_t __attribute__((ext_vector_type(4)));
+    f4_t* o = reinterpret_cast<f4_t*>(static_cast<float*>(ep.out) + (int64_t)row * ep.ldo + n);
+    const f4_t lo = {v.lo.x, v.lo.y, v.lo.z, v.lo.w}, hi = {v.hi.x, v.hi.y, v.hi.z, v.hi.w};
+    if constexpr (NT) {
+      __builtin_nontemporal_store(lo, o);
+      __builtin_nontemporal_store(hi, o + 1);
+    } else {
+      o[0] = lo;
+      o[1] = hi;
+    }
   }
 }
 

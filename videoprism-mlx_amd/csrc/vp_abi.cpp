@@ -670,15 +670,18 @@ int vp_dev_gemm_diag(int diag, const void* A, const void* W, int64_t M, int64_t 
   return VP_OK;
 }
 
-// Not in the public header: one named bf16 GEMM kernel (which = 4: gemm_bf16_w4, 8: gemm_bf16)
+// Not in the public header: one named bf16 GEMM kernel (which = 2: gemm_bf16_ov, 4: gemm_bf16_w4,
+// 8: gemm_bf16)
 // with any epilogue, for kernel A/B tests (tests/test_gpu_kernels.py) and tools/gemm_bench.py.
 // epi >= 1000 selects the 4-wave kernel's ablation builds.
 int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t M, int64_t N,
                        int64_t K, void* out, const float* bias, const void* resid, const float* pos,
                        int64_t pos_rows, const float* rowpad, void* stream) {
   using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
+  if (which != 2) {
+    const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+    if (e) return fail(VP_EINVAL, e);
+  }
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
   ep.pos = pos; ep.pos_rows = (int)(pos_rows > 0 ? pos_rows : 1); ep.rowpad = rowpad;
@@ -687,8 +690,12 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
     VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
   else if (which == 8)
     VP_HIP(gemm_bf16(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
-  else
-    return fail(VP_EINVAL, "which must be 4 or 8");
+  else if (which == 2) {
+    if (!gemm_bf16_ov_ok(epi >= 1000 ? 0 : epi, (int)M, (int)N, (int)K, K, K))
+      return fail(VP_EINVAL, "shape/epilogue not supported by gemm_bf16_ov");
+    VP_HIP(gemm_bf16_ov(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
+  } else
+    return fail(VP_EINVAL, "which must be 2, 4 or 8");
   return VP_OK;
 }
 

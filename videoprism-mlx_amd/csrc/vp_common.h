@@ -25,13 +25,31 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
+// two f32 -> packed bf16 (round to nearest even): one v_cvt_pk_bf16_f32 on gfx950
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_v __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_v{lo, hi}, bf16x2_t));
 }
 
 // Exact-erf GELU (layers.py:31).  erff from the device libm.
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+// nontemporal (streaming) stores of 8 / 16 bytes: outputs that the next kernel reads back from
+// HBM anyway go past L2 instead of being written back from it later
+typedef unsigned nt_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned nt_u32x4 __attribute__((ext_vector_type(4)));
+typedef float nt_f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_nt(void* p, uint2 v) {
+  __builtin_nontemporal_store(nt_u32x2{v.x, v.y}, reinterpret_cast<nt_u32x2*>(p));
+}
+__device__ __forceinline__ void st_nt(void* p, uint4 v) {
+  __builtin_nontemporal_store(nt_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_u32x4*>(p));
+}
+__device__ __forceinline__ void st_nt(void* p, float4 v) {
+  __builtin_nontemporal_store(nt_f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_f32x4*>(p));
 }
 
 __device__ __forceinline__ int wave_id() {

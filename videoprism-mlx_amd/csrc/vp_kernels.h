@@ -40,7 +40,12 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 // staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
-// picks gemm_bf16_w4 or gemm_bf16 by shape (VP_GEMM_KERNEL=w8|w4 overrides)
+// 4-wave, 256x128 tile, two accumulator sets: the epilogue of tile j runs under the MFMAs of
+// tile j+1 (gemm_bf16_ov.hip).  bf16-output epilogues, M % 256, N % 128, K % 64, K >= 704.
+bool gemm_bf16_ov_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw);
+hipError_t gemm_bf16_ov(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                        int N, int K, const EpiArgs& ep, hipStream_t s);
+// picks gemm_bf16_w4 or gemm_bf16 by shape (VP_GEMM_KERNEL=ov|w4|w8 overrides)
 hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                           int N, int K, const EpiArgs& ep, hipStream_t s);
 
