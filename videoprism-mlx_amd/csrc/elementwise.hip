@@ -59,7 +59,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         void* __restrict__ out, int perm, int T,
-                                                        int Nsp, const float* __restrict__ add) {
+                                                        int Nsp, const float* __restrict__ add,
+                                                        float* __restrict__ out_rs) {
   constexpr int D = NCH * 256;
   const int lane = threadIdx.x & 63;
   const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
       orow = ((int64_t)b * T + t) * Nsp + n;
       t_of_out = t;
     }
+    float4 ys[NCH];  // the stored values (bf16-rounded when OUT_BF16), for out_rs
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 256 + lane * 4;
@@ -144,13 +146,82 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
         y.x += a.x; y.y += a.y; y.z += a.z; y.w += a.w;
       }
       if constexpr (OUT_BF16) {
-        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + orow * D + col) =
-            make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+        const uint2 pk = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+        *reinterpret_cast<uint2*>(static_cast<bf16_t*>(out) + orow * D + col) = pk;
+        ys[c] = make_float4(__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                            __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u));
       } else {
         *reinterpret_cast<float4*>(static_cast<float*>(out) + orow * D + col) = y;
+        ys[c] = y;
       }
     }
+    if (out_rs) {  // statistics of the stored row for the LayerNorm folded into the next GEMM
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) a += (ys[c].x + ys[c].y) + (ys[c].z + ys[c].w);
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) a += __shfl_xor(a, off);
+      const float mean = a * (1.0f / D);
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const float dx = ys[c].x - mean, dy = ys[c].y - mean, dz = ys[c].z - mean, dw = ys[c].w - mean;
+        q += (dx * dx + dy * dy) + (dz * dz + dw * dw);
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+      const float rs = 1.0f / sqrtf(q * (1.0f / D) + 1e-6f);
+      if (lane == 0) *reinterpret_cast<float2*>(out_rs + 2 * orow) = make_float2(rs, -mean * rs);
+    }
   }
+}
+
+// ---- LayerNorm statistics for the GEMM-folded LayerNorm (EPI_*_LN) ----
+// partials: st[p][row] = (sum, M2) over columns [128p, 128p+128) of the stored bf16 row
+__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ st, int P,
+                                                                int64_t M, float* __restrict__ rs_out) {
+  const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (row >= M) return;
+  float S[16], Q[16];
+  float tot = 0.f;
+  for (int p = 0; p < P; ++p) {
+    const float2 v = *reinterpret_cast<const float2*>(st + 2 * ((int64_t)p * M + row));
+    S[p] = v.x;
+    Q[p] = v.y;
+    tot += v.x;
+  }
+  const float D = 128.0f * P;
+  const float mean = tot / D;
+  float m2 = 0.f;
+  for (int p = 0; p < P; ++p) {  // Chan: M2 = sum Q_p + n_p (mean_p - mean)^2
+    const float d = S[p] * (1.0f / 128.0f) - mean;
+    m2 += Q[p] + 128.0f * d * d;
+  }
+  const float rs = 1.0f / sqrtf(m2 / D + 1e-6f);
+  *reinterpret_cast<float2*>(rs_out + 2 * row) = make_float2(rs, -mean * rs);
+}
+
+// two-pass statistics straight from bf16 rows, one wave per row
+__global__ __launch_bounds__(256) void ln_row_stats_kernel(const bf16_t* __restrict__ x, int64_t M, int D,
+                                                           float* __restrict__ rs_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* r = x + row * D;
+  float a = 0.f;
+  for (int c = lane; c < D; c += 64) a += bf2f(r[c]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) a += __shfl_xor(a, off);
+  const float mean = a / D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float d = bf2f(r[c]) - mean;
+    q += d * d;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+  const float rs = 1.0f / sqrtf(q / D + 1e-6f);
+  if (lane == 0) *reinterpret_cast<float2*>(rs_out + 2 * row) = make_float2(rs, -mean * rs);
 }
 
 __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x,
@@ -215,23 +286,24 @@ int grid_for(int64_t work, int block) {
 
 template <int NCH>
 hipError_t ln_launch(const void* x, int in_is_bf16, int rows, const float* gamma, const float* beta,
-                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add, hipStream_t s) {
+                     void* out, int out_is_bf16, int perm, int T, int Nsp, const float* add, hipStream_t s,
+                     float* out_rs) {
   constexpr int RPW = NCH <= 4 ? 4 : 2;  // rows per wave
   const dim3 grid((rows + 4 * RPW - 1) / (4 * RPW));
   if (in_is_bf16) {
     if (out_is_bf16)
       hipLaunchKernelGGL((layernorm_kernel<NCH, true, true, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
-                         out, perm, T, Nsp, add);
+                         out, perm, T, Nsp, add, out_rs);
     else
       hipLaunchKernelGGL((layernorm_kernel<NCH, false, true, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
-                         out, perm, T, Nsp, add);
+                         out, perm, T, Nsp, add, out_rs);
   } else {
     if (out_is_bf16)
       hipLaunchKernelGGL((layernorm_kernel<NCH, true, false, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
-                         out, perm, T, Nsp, add);
+                         out, perm, T, Nsp, add, out_rs);
     else
       hipLaunchKernelGGL((layernorm_kernel<NCH, false, false, RPW>), grid, dim3(256), 0, s, x, rows, gamma, beta,
-                         out, perm, T, Nsp, add);
+                         out, perm, T, Nsp, add, out_rs);
   }
   return hipGetLastError();
 }
@@ -263,17 +335,29 @@ hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is
 
 hipError_t layernorm(const void* x, int in_is_bf16, int rows, int D, const float* gamma,
                      const float* beta, void* out, int out_is_bf16, int perm, int T, int Nsp,
-                     const float* add, hipStream_t s) {
+                     const float* add, hipStream_t s, float* out_rs) {
   switch (D) {
-    case 256: return ln_launch<1>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 512: return ln_launch<2>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 768: return ln_launch<3>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 1024: return ln_launch<4>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 1280: return ln_launch<5>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 1536: return ln_launch<6>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
-    case 2048: return ln_launch<8>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s);
+    case 256: return ln_launch<1>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
+    case 512: return ln_launch<2>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
+    case 768: return ln_launch<3>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
+    case 1024: return ln_launch<4>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
+    case 1280: return ln_launch<5>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
+    case 1536: return ln_launch<6>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
+    case 2048: return ln_launch<8>(x, in_is_bf16, rows, gamma, beta, out, out_is_bf16, perm, T, Nsp, add, s, out_rs);
   }
   return hipErrorInvalidValue;
+}
+
+hipError_t ln_stats_finalize(const float* st_part, int P, int64_t M, float* ln_rs, hipStream_t s) {
+  if (P < 1 || P > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, st_part, P, M,
+                     ln_rs);
+  return hipGetLastError();
+}
+
+hipError_t ln_row_stats(const bf16_t* x, int64_t M, int D, float* ln_rs, hipStream_t s) {
+  hipLaunchKernelGGL(ln_row_stats_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, M, D, ln_rs);
+  return hipGetLastError();
 }
 
 hipError_t cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s) {

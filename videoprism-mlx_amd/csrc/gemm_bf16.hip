@@ -413,6 +413,7 @@ hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W
   const bool w4_ok = (uint64_t)M * (uint64_t)lda * 2 < 0xFFFFFFF0ull &&
                      (uint64_t)N * (uint64_t)ldw * 2 < 0xFFFFFFF0ull;
   bool use_w4 = w4_ok;
+  if (epi >= EPI_BF16_LN) return w4_ok ? gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s) : hipErrorInvalidValue;
   if (mode == 8) use_w4 = false;
   else if (mode != 4 && (epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024) use_w4 = false;
   if (use_w4) return gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s);

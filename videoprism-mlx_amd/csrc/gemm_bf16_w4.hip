@@ -241,6 +241,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     // retires in issue order, so a bias load issued in the epilogue would wait for the next
     // tile's prefetch
     float4 bl[2], bh[2];
+    float4 cl[2], ch[2];  // EPI_*_LN: column sums of W'
+    float2 rs[8][2];      // EPI_*_LN: (rstd, -mean*rstd) of rows mt*16 + pass*8 + er
     {
       const int tile = first + j * stride;
       const int nb = (tile % tilesN) * BN + wn * 128 + es * 8;
@@ -248,6 +250,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       for (int nh = 0; nh < 2; ++nh) {
         bl[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64);
         bh[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64 + 4);
+      }
+      if constexpr (EpiTraits<EPI>::kLn) {
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh) {
+          cl[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64);
+          ch[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64 + 4);
+        }
+        const int mb = (tile / tilesN) * BM + wm * 128 + er;
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass)
+            rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
     h0(g & 1, true);
@@ -289,6 +304,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       for (int q = 0; q < 4; ++q)
         *reinterpret_cast<f32x4*>(sb + (((q * 4 + (lane >> 4)) ^ (frow & 7)) << 4)) = acc[nh * 4 + q][mt];
     };
+    // EPI_*_ST: the stored row values of block (mt, nh=0), then per (mt, pass) the row's
+    // partial over this wave's 128 columns: sum and sum of squares about the partial mean
+    // (two passes over the 16 values a lane holds, each reduced over the row's 8 lanes); lane
+    // es keeps the partials of mt == es, so the wave stores its 128 rows with 2 instructions
+    float sv[2][8];
+    float pS[2] = {0.f, 0.f}, pQ[2] = {0.f, 0.f};
     if constexpr (Tr::kExtra) fetch(0, 0);
     put(0);
 #pragma unroll
@@ -307,8 +328,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         F8 v;
         v.lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
         v.hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
-        v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
-        v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
+        if constexpr (Tr::kLn) {  // LN(x) . W + b = rstd * (x . W') - mean*rstd * c + b'
+          const float r = rs[mt][pass].x, q = rs[mt][pass].y;
+          v.lo.x = fmaf(r, v.lo.x, fmaf(q, cl[nh].x, bl[nh].x));
+          v.lo.y = fmaf(r, v.lo.y, fmaf(q, cl[nh].y, bl[nh].y));
+          v.lo.z = fmaf(r, v.lo.z, fmaf(q, cl[nh].z, bl[nh].z));
+          v.lo.w = fmaf(r, v.lo.w, fmaf(q, cl[nh].w, bl[nh].w));
+          v.hi.x = fmaf(r, v.hi.x, fmaf(q, ch[nh].x, bh[nh].x));
+          v.hi.y = fmaf(r, v.hi.y, fmaf(q, ch[nh].y, bh[nh].y));
+          v.hi.z = fmaf(r, v.hi.z, fmaf(q, ch[nh].z, bh[nh].z));
+          v.hi.w = fmaf(r, v.hi.w, fmaf(q, ch[nh].w, bh[nh].w));
+        } else {
+          v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
+          v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
+        }
         float keep = 1.0f;
         if constexpr (Tr::kKeep) {
           if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
@@ -317,9 +350,41 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           if (ep.ldo == -12345) epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
           else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
         } else {
-          epi_store8<EPI, !(DIAG & 256)>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          const epi_u32x4 pk = epi_store8<EPI, !(DIAG & 256)>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          if constexpr (Tr::kStats) {
+            float y[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              y[2 * i] = __uint_as_float(pk[i] << 16);
+              y[2 * i + 1] = __uint_as_float(pk[i] & 0xffff0000u);
+            }
+            if (nh == 0) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) sv[pass][i] = y[i];
+            } else {
+              float s0 = 0.f;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) s0 += sv[pass][i] + y[i];
+              const float S = sum8_lanes(s0);
+              const float mp = S * (1.0f / 128.0f);
+              float q0 = 0.f;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const float a = sv[pass][i] - mp, b2 = y[i] - mp;
+                q0 = fmaf(a, a, fmaf(b2, b2, q0));
+              }
+              const float Q = sum8_lanes(q0);
+              if (es == mt) { pS[pass] = S; pQ[pass] = Q; }
+            }
+          }
         }
       }
+    }
+    if constexpr (Tr::kStats) {
+      const int p = (n0 >> 7);  // 128-column partial index of this wave
+      float* dst = ep.st_part + 2 * ((int64_t)p * ep.st_rows + m0 + es * 16 + er);
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) *reinterpret_cast<float2*>(dst + 16 * pass) = make_float2(pS[pass], pQ[pass]);
     }
   }
   // drain the tail's (clamped) loads before the workgroup's LDS is released
@@ -403,6 +468,11 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
     case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16: return launch_w4<EPI_POS_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN_BF16: return launch_w4<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_BF16_LN: return launch_w4<EPI_BF16_LN>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_GELU_BF16_LN: return launch_w4<EPI_GELU_BF16_LN>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16_ST: return launch_w4<EPI_RESID_FFN_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

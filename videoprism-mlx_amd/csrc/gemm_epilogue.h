@@ -18,10 +18,13 @@ namespace vp {
 
 template <int EPI>
 struct EpiTraits {
-  static constexpr bool kGelu = EPI == EPI_GELU_BF16;
+  static constexpr bool kLn = EPI == EPI_BF16_LN || EPI == EPI_GELU_BF16_LN;
+  static constexpr bool kStats = EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST || EPI == EPI_POS_BF16_ST;
+  static constexpr bool kGelu = EPI == EPI_GELU_BF16 || EPI == EPI_GELU_BF16_LN;
   static constexpr bool kResidF32 = EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN;
-  static constexpr bool kResidBf16 = EPI == EPI_RESID_BF16 || EPI == EPI_RESID_FFN_BF16;
-  static constexpr bool kPos = EPI == EPI_POS_F32 || EPI == EPI_POS_BF16;
+  static constexpr bool kResidBf16 = EPI == EPI_RESID_BF16 || EPI == EPI_RESID_FFN_BF16 ||
+                                     EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST;
+  static constexpr bool kPos = EPI == EPI_POS_F32 || EPI == EPI_POS_BF16 || EPI == EPI_POS_BF16_ST;
   static constexpr bool kExtra = kResidF32 || kResidBf16 || kPos;
   static constexpr bool kKeep = kGelu || kResidF32 || kResidBf16;
   static constexpr bool kOutBf16 = !(EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN || EPI == EPI_POS_F32);
@@ -144,14 +147,16 @@ typedef unsigned epi_u32x4 __attribute__((ext_vector_type(4)));
 // NT: nontemporal output stores (global_store ... nt).  Measured on the w4 kernel at the
 // encoder's shapes: qkv 432 -> 379 us, post 147 -> 130 us, ffn1 579 -> 502 us (the output
 // streams past L2 instead of being written back from it later; tools/gemm_bench.py nt).
+// returns the stored bf16 values (packed) for the row-statistics epilogues
 template <int EPI, bool NT = true>
-__device__ __forceinline__ void epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
+__device__ __forceinline__ epi_u32x4 epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
   using Tr = EpiTraits<EPI>;
   v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra);
   v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra);
+  epi_u32x4 pk = {0u, 0u, 0u, 0u};
   if constexpr (Tr::kOutBf16) {
-    const epi_u32x4 pk = {pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
-                          pack_bf16x2(v.hi.z, v.hi.w)};
+    pk = epi_u32x4{pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
+                   pack_bf16x2(v.hi.z, v.hi.w)};
     epi_u32x4* dst = reinterpret_cast<epi_u32x4*>(static_cast<bf16_t*>(ep.out) + (int64_t)row * ep.ldo + n);
     if constexpr (NT) __builtin_nontemporal_store(pk, dst);
     else *dst = pk;
@@ -167,6 +172,15 @@ __device__ __forceinline__ void epi_store8(const EpiArgs& ep, int row, int n, F8
       o[1] = hi;
     }
   }
+  return pk;
+}
+
+// sum over the 8 consecutive lanes (lane & ~7) of a wave; every lane gets the same bits
+__device__ __forceinline__ float sum8_lanes(float x) {
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  return x;
 }
 
 }  // namespace vp

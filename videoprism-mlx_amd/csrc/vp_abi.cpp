@@ -82,6 +82,10 @@ struct LayerW {  // one transformer layer, packed
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
   void* w1 = nullptr;    // [F][D]
   float* b1 = nullptr;
+  // bf16 handles fold LN1 / LN2 into the consuming GEMM (EPI_*_LN): wqkv / w1 hold
+  // W' = W diag(1+scale), bqkv / b1 hold b + W beta, and c = row sums of bf16(W')
+  float* cqkv = nullptr;
+  float* c1 = nullptr;
   void* w2 = nullptr;    // [D][F]
   float* b2 = nullptr;
 };
@@ -207,6 +211,30 @@ void build_expected(vp_handle* h) {
 
 const std::vector<float>& param_data(vp_handle* h, const std::string& n) { return h->host.at(n).data; }
 
+// LayerNorm folded into the following GEMM (bf16 handles): w [N][K] *= gamma[k],
+// b[n] += sum_k w[n][k] beta[k] (before scaling, fp64), c[n] = sum_k bf16(w'[n][k]) (fp64).
+// LN(x).W + b = rstd * (x.W') - mean*rstd * c + b'   (layers.py:208-270 with :273-313)
+std::vector<float> fold_ln(std::vector<float>& w, std::vector<float>& b, const std::vector<float>& gamma,
+                           const std::vector<float>& beta, int64_t N, int64_t K) {
+  std::vector<float> c(N);
+  for (int64_t n = 0; n < N; ++n) {
+    double bb = b[n], cs = 0.0;
+    float* row = w.data() + (size_t)n * K;
+    for (int64_t k = 0; k < K; ++k) {
+      bb += (double)row[k] * beta[k];
+      row[k] = row[k] * gamma[k];
+      const uint16_t r = host_f2bf(row[k]);
+      uint32_t u = (uint32_t)r << 16;
+      float rf;
+      std::memcpy(&rf, &u, 4);
+      cs += rf;
+    }
+    b[n] = (float)bb;
+    c[n] = (float)cs;
+  }
+  return c;
+}
+
 int pack_stack(vp_handle* h, const std::string& stack, int L, std::vector<LayerW>& out) {
   const int64_t D = h->cfg.model_dim, F = h->cfg.mlp_dim;
   const float qscale = 1.0f / std::sqrt((float)(D / h->cfg.num_heads));  // layers.py:576-583
@@ -240,11 +268,6 @@ int pack_stack(vp_handle* h, const std::string& stack, int L, std::vector<LayerW
       for (int64_t n = 0; n < D; ++n) tb[(size_t)which * D + n] = b[n] * sc;
     }
     int rc;
-    if ((rc = upload_mat(h, t, &lw.wqkv)) || (rc = upload_f32(h, tb, &lw.bqkv))) return rc;
-    // post: w[d][n][h] is already [out D][in N*H]
-    std::vector<float> wp(wpost.begin() + (size_t)l * D * D, wpost.begin() + (size_t)(l + 1) * D * D);
-    std::vector<float> bp(bpost.begin() + (size_t)l * D, bpost.begin() + (size_t)(l + 1) * D);
-    if ((rc = upload_mat(h, wp, &lw.wpost)) || (rc = upload_f32(h, bp, &lw.bpost))) return rc;
     std::vector<float> g1(D), be1(D), g2(D), be2(D);
     for (int64_t i = 0; i < D; ++i) {
       g1[i] = lng[(size_t)l * D + i] + 1.0f;   // direct_scale=False (layers.py:259-260)
@@ -252,6 +275,15 @@ int pack_stack(vp_handle* h, const std::string& stack, int L, std::vector<LayerW
       g2[i] = ln2g[(size_t)l * D + i] + 1.0f;
       be2[i] = ln2b[(size_t)l * D + i];
     }
+    if (is_bf16(h)) {
+      const std::vector<float> c = fold_ln(t, tb, g1, be1, 3 * D, D);
+      if ((rc = upload_f32(h, c, &lw.cqkv))) return rc;
+    }
+    if ((rc = upload_mat(h, t, &lw.wqkv)) || (rc = upload_f32(h, tb, &lw.bqkv))) return rc;
+    // post: w[d][n][h] is already [out D][in N*H]
+    std::vector<float> wp(wpost.begin() + (size_t)l * D * D, wpost.begin() + (size_t)(l + 1) * D * D);
+    std::vector<float> bp(bpost.begin() + (size_t)l * D, bpost.begin() + (size_t)(l + 1) * D);
+    if ((rc = upload_mat(h, wp, &lw.wpost)) || (rc = upload_f32(h, bp, &lw.bpost))) return rc;
     if ((rc = upload_f32(h, g1, &lw.ln1_g)) || (rc = upload_f32(h, be1, &lw.ln1_b)) ||
         (rc = upload_f32(h, g2, &lw.ln2_g)) || (rc = upload_f32(h, be2, &lw.ln2_b)))
       return rc;
@@ -264,6 +296,10 @@ int pack_stack(vp_handle* h, const std::string& stack, int L, std::vector<LayerW
       for (int64_t n = 0; n < D; ++n) t2[(size_t)n * F + k] = w2l[k * D + n];
     std::vector<float> bb1(b1.begin() + (size_t)l * F, b1.begin() + (size_t)(l + 1) * F);
     std::vector<float> bb2(b2.begin() + (size_t)l * D, b2.begin() + (size_t)(l + 1) * D);
+    if (is_bf16(h)) {
+      const std::vector<float> c = fold_ln(t1, bb1, g2, be2, F, D);
+      if ((rc = upload_f32(h, c, &lw.c1))) return rc;
+    }
     if ((rc = upload_mat(h, t1, &lw.w1)) || (rc = upload_f32(h, bb1, &lw.b1)) ||
         (rc = upload_mat(h, t2, &lw.w2)) || (rc = upload_f32(h, bb2, &lw.b2)))
       return rc;
@@ -273,7 +309,7 @@ int pack_stack(vp_handle* h, const std::string& stack, int L, std::vector<LayerW
 
 // workspace carve-up (all offsets 256-B aligned)
 struct WsLayout {
-  size_t x = 0, x2 = 0, hbuf = 0, big = 0, pad_btn = 0, pad_bnt = 0, total = 0;
+  size_t x = 0, x2 = 0, hbuf = 0, big = 0, pad_btn = 0, pad_bnt = 0, st_part = 0, ln_rs = 0, total = 0;
 };
 
 size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -296,6 +332,9 @@ WsLayout ws_layout(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t 
   L.big = off; off = align256(off + (size_t)M * bigcols * es);
   L.pad_btn = off; off = align256(off + (size_t)M * 4);
   L.pad_bnt = off; off = align256(off + (size_t)M * 4);
+  // GEMM-folded LayerNorm (bf16): per-row partial statistics and (rstd, -mean*rstd)
+  L.st_part = off; off = align256(off + (size_t)(D / 128) * M * 8);
+  L.ln_rs = off; off = align256(off + (size_t)M * 8);
   L.total = off;
   return L;
 }
@@ -495,12 +534,18 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
     pad_bnt = reinterpret_cast<float*>(ws + L.pad_bnt);
     VP_HIP(expand_paddings(frame_paddings, (int)B, (int)T, Nsp, pad_btn, pad_bnt, s));
   }
+  // bf16: LayerNorms inside the layers are folded into the consuming GEMMs (EPI_*_LN); the
+  // residual-stream producers emit row statistics (EPI_*_ST) that ln_stats_finalize turns into
+  // (rstd, -mean*rstd) per row
+  float* st_part = reinterpret_cast<float*>(ws + L.st_part);
+  float* ln_rs = reinterpret_cast<float*>(ws + L.ln_rs);
   auto gemm = [&](int epi, const void* A, int K, const void* Wt, int N, void* o, int64_t ldo,
                   const float* bias, const void* resid, const float* pos, int pos_rows,
-                  const float* rowpad) -> hipError_t {
+                  const float* rowpad, const float* lnc = nullptr) -> hipError_t {
     EpiArgs ep;
     ep.out = o; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldo;
     ep.pos = pos; ep.pos_rows = pos_rows; ep.rowpad = rowpad;
+    ep.ln_rs = ln_rs; ep.ln_c = lnc; ep.st_part = st_part; ep.st_rows = M;
     if (bf) return gemm_bf16_auto(epi, (const bf16_t*)A, K, (const bf16_t*)Wt, K, M, N, K, ep, s);
     return gemm_f32(epi, (const float*)A, K, (const float*)Wt, K, M, N, K, ep, s);
   };
@@ -531,32 +576,57 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   const double kreal = (double)P_ * P_ * 3;
   VP_HIP(rec(PC_PATCHIFY, 0.0, dM * kreal * (in_dtype == VP_BF16 ? 2 : 4) + dM * h->kpad * dE, [&] {
     return patchify(video, in_dtype == VP_BF16, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
+  const bool fold = bf && c.num_spatial_layers > 0;  // LN1 of spatial layer 0 folded
   VP_HIP(rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, dE, 0), [&] {
-    return gemm(epi_pos, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr, h->spatial_pos, Nsp, nullptr); }));
+    return gemm(fold ? EPI_POS_BF16_ST : epi_pos, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr,
+                h->spatial_pos, Nsp, nullptr); }));
   const double ln_bytes = dM * dD * dE + dM * dD * dE;
+  const double fin_bytes = dM * (D / 128) * 8.0 + dM * 8.0;
+  auto finalize = [&]() {
+    return rec(PC_LAYERNORM, 0.0, fin_bytes, [&] { return ln_stats_finalize(st_part, D / 128, M, ln_rs, s); });
+  };
+  if (fold) VP_HIP(finalize());
 
   auto run_stack = [&](std::vector<LayerW>& layers, void* xs, int num_seq, int S,
                        const float* pad) -> int {
     const int acls = num_seq == (int)(B * T) ? PC_ATTN_SPATIAL : PC_ATTN_TEMPORAL;
     const double aflops = 4.0 * num_seq * (double)S * S * dD;
     const double abytes = dM * 3 * dD * dE + dM * dD * dE;
-    for (auto& lw : layers) {
-      VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
-        return layernorm(xs, bf, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
-      VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
-        return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
+    for (size_t li = 0; li < layers.size(); ++li) {
+      LayerW& lw = layers[li];
+      const bool last = li + 1 == layers.size();
+      if (bf) {  // LN1 folded: A = the residual stream, (rstd, -mean*rstd) in ln_rs
+        VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
+          return gemm(EPI_BF16_LN, xs, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr,
+                      lw.cqkv); }));
+      } else {
+        VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
+          return layernorm(xs, bf, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
+        VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
+          return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
+      }
       VP_HIP(rec(acls, aflops, abytes, [&] {
         if (!bf) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s);
         if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, c.atten_logit_cap, pad, s);
         return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, c.atten_logit_cap, pad, s); }));
       VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {
-        return gemm(epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1, nullptr); }));
-      VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
-        return layernorm(xs, bf, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
-      VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
-        return gemm(EPI_GELU_BF16, hb, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad); }));
+        return gemm(bf ? EPI_RESID_BF16_ST : epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1,
+                    nullptr); }));
+      if (bf) {  // LN2 folded into ffn_layer1
+        VP_HIP(finalize());
+        VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
+          return gemm(EPI_GELU_BF16_LN, xs, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad, lw.c1); }));
+      } else {
+        VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
+          return layernorm(xs, bf, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
+        VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
+          return gemm(EPI_GELU_BF16, hb, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad); }));
+      }
+      const bool st = bf && !last;  // the next layer's LN1 statistics
       VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, dE, dE), [&] {
-        return gemm(epi_resid_ffn, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1, pad); }));
+        return gemm(st ? EPI_RESID_FFN_BF16_ST : epi_resid_ffn, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1,
+                    pad); }));
+      if (st) VP_HIP(finalize());
     }
     return VP_OK;
   };
@@ -568,7 +638,8 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
       return layernorm(x, bf, M, D, h->sln_g, h->sln_b, spatial_out, out_dtype == VP_BF16, PERM_NONE, 1, 1, nullptr, s); }));
   const float* tpos = h->temporal_pos + (size_t)T * kMaxT * D;
   VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
-    return layernorm(x, bf, M, D, h->sln_g, h->sln_b, x2, bf, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s); }));
+    return layernorm(x, bf, M, D, h->sln_g, h->sln_b, x2, bf, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s,
+                     bf && c.num_temporal_layers > 0 ? ln_rs : nullptr); }));
   // 4. temporal encoder over (b n) sequences of T tokens
   if ((rc = run_stack(h->temporal, x2, (int)(B * Nsp), (int)T, pad_bnt))) return rc;
   // 5. temporal_ln and '(bn)td->b(tn)d'

@@ -18,6 +18,17 @@ enum Epilogue {
   EPI_RESID_BF16 = 5,
   EPI_POS_BF16 = 6,
   EPI_RESID_FFN_BF16 = 7,
+  // LayerNorm folded into the consuming GEMM (bf16 path): A = the raw residual stream x,
+  // W' = diag(1+scale) W, bias' = b + W.beta, and per row (rstd, -mean*rstd) from ln_rs:
+  //   out = rstd * acc + (-mean*rstd) * c[n] + bias'[n],   c[n] = sum_k W'[n][k]
+  EPI_BF16_LN = 8,       // as EPI_BF16   (q|k|v of LN1(x))
+  EPI_GELU_BF16_LN = 9,  // as EPI_GELU   (ffn_layer1 of LN2(x))
+  // residual-stream producers that also emit the row statistics of the bf16 values they
+  // store: per 128-column partial p = (n / 128), st_part[p][row] = (sum, sum of squares about
+  // the partial mean); ln_stats_finalize() combines them into ln_rs
+  EPI_RESID_BF16_ST = 10,
+  EPI_RESID_FFN_BF16_ST = 11,
+  EPI_POS_BF16_ST = 12,
 };
 
 struct EpiArgs {
@@ -29,6 +40,10 @@ struct EpiArgs {
   const float* pos = nullptr;     // EPI_POS_F32: [pos_rows][N]
   int pos_rows = 1;
   const float* rowpad = nullptr;  // optional [M], 1 = padded token
+  const float* ln_rs = nullptr;   // EPI_*_LN: [M][2] (rstd, -mean*rstd)
+  const float* ln_c = nullptr;    // EPI_*_LN: [N] column sums of W'
+  float* st_part = nullptr;       // EPI_*_ST: [N/128][M][2] partial (sum, M2) of each row
+  int64_t st_rows = 0;            // EPI_*_ST: M (partial stride)
 };
 
 // ---- bf16 MFMA GEMM (gemm_bf16.hip) ----
@@ -75,14 +90,22 @@ hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is
                     int H, int W, int C, int P, int kpad, hipStream_t s);
 // LayerNorm over D of fp32 or bf16 rows; gamma already holds (1 + scale).  Output row r goes
 // to row perm(r); `add` (optional, fp32 [add_rows][D]) is added by the *output* row's t index.
+// out_rs (optional): (rstd, -mean*rstd) of each stored output row (as ln_rs above), by
+// output row index
 hipError_t layernorm(const void* x, int in_is_bf16, int rows, int D, const float* gamma,
                      const float* beta, void* out, int out_is_bf16, int perm, int T, int Nsp,
-                     const float* add, hipStream_t s);
+                     const float* add, hipStream_t s, float* out_rs = nullptr);
 // fp32 -> bf16 cast (weights are pre-packed on the host; this is for activations)
 hipError_t cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s);
 // per-token padding vector expansion: frame_pad [B*T] -> token pads in both orders
 hipError_t expand_paddings(const float* frame_pad, int B, int T, int Nsp, float* pad_btn,
                            float* pad_bnt, hipStream_t s);
+
+// (rstd, -mean*rstd) of every row from the P partial (sum, M2) pairs of 128 columns each
+// (Chan's combination), D = 128 * P, LayerNorm eps 1e-6 (layers.py:240-243)
+hipError_t ln_stats_finalize(const float* st_part, int P, int64_t M, float* ln_rs, hipStream_t s);
+// same statistics straight from bf16 rows [M][D] (two-pass), for tests and the op API
+hipError_t ln_row_stats(const bf16_t* x, int64_t M, int D, float* ln_rs, hipStream_t s);
 
 hipError_t pool_l2(const void* emb, int is_bf16, int B, int L, int D, float* out, hipStream_t s);
 
