@@ -336,3 +336,88 @@ def test_pool_l2(cuda):
     m = e.double().mean(1)
     ref = m / torch.sqrt((m * m).sum(-1, keepdim=True) + 1e-12)
     assert float((out.double() - ref).abs().max()) < 1e-6
+
+
+# ---- GEMM-folded LayerNorm (bf16 forward): EPI_*_LN consumers and EPI_*_ST producers ----
+
+def _ln_ref(x, gamma1p, beta):
+    """layers.py:208-270 in fp64: (x - mean) * rsqrt(var + 1e-6) * (1 + scale) + bias."""
+    m = x.mean(-1, keepdim=True)
+    v = ((x - m) ** 2).mean(-1, keepdim=True)
+    return (x - m) / torch.sqrt(v + 1e-6) * gamma1p + beta
+
+
+@pytest.mark.parametrize("epi", [nat.EPI_BF16_LN, nat.EPI_GELU_LN])
+@pytest.mark.parametrize("M,N,K", [(1024, 2304, 768), (512, 3072, 768), (256, 1024, 1024)])
+def test_gemm_ln_fold(cuda, epi, M, N, K):
+    """LN(x).W + b computed as rstd*(x.W') - mean*rstd*c + b' with W' = W diag(gamma),
+    b' = b + W.beta, c = row sums of bf16(W') -- against LN then GEMM in fp64 on the same bf16
+    x.  The fold skips the reference's bf16 rounding of LN(x), so the bound is the bf16
+    rounding of W' and of the output (rtol 2^-7) plus 2e-3 abs."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    x = _bf(torch.randn(M, K, generator=g) * 2 + 0.5)          # mean offset: exercises -mean*c
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g) * 0.1
+    gam = 1 + torch.randn(K, generator=g) * 0.1
+    bet = torch.randn(K, generator=g) * 0.1
+    pad = (torch.rand(M, generator=g) < 0.2).float()
+    wp = _bf(w * gam)
+    c = wp.double().sum(1).float()
+    bp = (b.double() + w.double() @ bet.double()).float()
+    rs = torch.empty(M, 2, device=cuda)
+    nat.dev_ln_stats(x.to(cuda), M, K, rs, from_partials=False)
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    nat.dev_gemm_ln(x.to(cuda), wp.to(cuda), bp.to(cuda), epi, out, ln_rs=rs, ln_c=c.to(cuda),
+                    rowpad=pad.to(cuda) if epi == nat.EPI_GELU_LN else None)
+    torch.cuda.synchronize()
+    # (1) the kernel's arithmetic: the folded form with the bf16 W' it is given, in fp64
+    xd = x.double()
+    mu, var = xd.mean(1, keepdim=True), xd.var(1, unbiased=False, keepdim=True)
+    rstd = 1 / torch.sqrt(var + 1e-6)
+    y = rstd * (xd @ wp.double().T - mu * c.double()) + bp.double()
+    # (2) the algebra: LayerNorm then GEMM with the unrounded weights (bf16 W' differs from W
+    # by one rounding, so this bound is looser)
+    y2 = _ln_ref(xd, gam.double(), bet.double()) @ w.double().T + b.double()
+    if epi == nat.EPI_GELU_LN:
+        keep = (1 - pad.double())[:, None]
+        y = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) * keep
+        y2 = 0.5 * y2 * (1 + torch.erf(y2 / 2 ** 0.5)) * keep
+    o = out.cpu().double()
+    err = (o - y).abs()
+    assert bool((err <= 2 ** -8 * y.abs() + 1e-4).all()), float(err.max())
+    err2 = (o - y2).abs()
+    assert float(err2.mean()) <= 2e-3 and float(err2.max()) <= 5e-2, (float(err2.mean()), float(err2.max()))
+
+
+@pytest.mark.parametrize("epi", [nat.EPI_RESID_BF16_ST, nat.EPI_RESID_FFN_BF16_ST, nat.EPI_POS_BF16_ST])
+def test_gemm_row_stats(cuda, epi):
+    """A residual-stream producer's partial row statistics, finalised, equal the two-pass
+    statistics of the bf16 rows it stored (ln_row_stats), and its stored values equal the
+    plain epilogue's bit for bit."""
+    M, N, K = 2048, 768, 768
+    g = torch.Generator(device="cpu").manual_seed(epi)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    x0 = (torch.randn(M, N, generator=g) * 3 + 1).to(cuda).to(torch.bfloat16)
+    pos = torch.randn(256, N, generator=g).to(cuda) if epi == nat.EPI_POS_BF16_ST else None
+    resid = epi != nat.EPI_POS_BF16_ST
+    plain = {nat.EPI_RESID_BF16_ST: nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16_ST: nat.EPI_RESID_FFN_BF16,
+             nat.EPI_POS_BF16_ST: nat.EPI_POS_BF16}[epi]
+    o_st = x0.clone() if resid else torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    part = torch.full((N // 128, M, 2), float("nan"), device=cuda)
+    nat.dev_gemm_ln(a, w, b, epi, o_st, resid=o_st if resid else None, pos=pos, st_part=part)
+    o_pl = x0.clone() if resid else torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    nat.dev_gemm_kernel(4, a, w, b, plain, o_pl, resid=o_pl if resid else None, pos=pos)
+    rs_p = torch.empty(M, 2, device=cuda)
+    rs_r = torch.empty(M, 2, device=cuda)
+    nat.dev_ln_stats(part, M, N, rs_p, from_partials=True)
+    nat.dev_ln_stats(o_st, M, N, rs_r, from_partials=False)
+    torch.cuda.synchronize()
+    assert torch.equal(o_st, o_pl)
+    xd = o_st.double()
+    mean, var = xd.mean(1), xd.var(1, unbiased=False)
+    rstd = 1 / torch.sqrt(var + 1e-6)
+    ref = torch.stack([rstd, -mean * rstd], 1)
+    assert torch.allclose(rs_p.double(), ref, rtol=2e-5, atol=1e-5)
+    assert torch.allclose(rs_r.double(), ref, rtol=2e-5, atol=1e-5)

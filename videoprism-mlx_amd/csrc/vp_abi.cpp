@@ -770,6 +770,36 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
   return VP_OK;
 }
 
+// Not in the public header: the GEMM-folded LayerNorm pieces (tests/test_gpu_kernels.py).
+// vp_dev_gemm_ln: EPI_BF16_LN / EPI_GELU_BF16_LN with (rstd, -mean*rstd) rows ln_rs and column
+// sums ln_c, or EPI_*_ST writing partial row statistics to st_part ([N/128][M][2]).
+int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
+                   const float* bias, const void* resid, const float* pos, int64_t pos_rows,
+                   const float* rowpad, const float* ln_rs, const float* ln_c, float* st_part,
+                   void* stream) {
+  using namespace vp;
+  if (epi < EPI_BF16_LN || epi > EPI_POS_BF16_ST) return fail(VP_EINVAL, "epilogue must be 8..12");
+  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  if (e) return fail(VP_EINVAL, e);
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
+  ep.pos = pos; ep.pos_rows = (int)(pos_rows > 0 ? pos_rows : 1); ep.rowpad = rowpad;
+  ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.st_part = st_part; ep.st_rows = M;
+  VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
+                      static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
+// which = 0: ln_stats_finalize(src = st_part [D/128][M][2]); 1: ln_row_stats(src = bf16 [M][D])
+int vp_dev_ln_stats(int which, const void* src, int64_t M, int64_t D, float* ln_rs, void* stream) {
+  using namespace vp;
+  if (D % 128 || D < 128) return fail(VP_EINVAL, "D must be a multiple of 128");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (which == 0) VP_HIP(ln_stats_finalize((const float*)src, (int)(D / 128), M, ln_rs, s));
+  else VP_HIP(ln_row_stats((const bf16_t*)src, M, (int)D, ln_rs, s));
+  return VP_OK;
+}
+
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
                     int64_t heads, float cap, const float* key_pad, void* stream) {
   using namespace vp;

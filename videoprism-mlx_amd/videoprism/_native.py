@@ -81,6 +81,10 @@ _SIGNATURES = {
     "vp_dev_gemm_kernel": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
                                    c_void_p]),
+    "vp_dev_gemm_ln": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
+                               c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p]),
+    "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
 }
 
 _lib = None
@@ -176,6 +180,27 @@ def dev_gemm_kernel(which, a, w, bias, epilogue, out, resid=None, pos=None, rowp
     call("vp_dev_gemm_kernel", which, epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias),
          _ptr(resid), _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad),
          _stream(stream))
+    return out
+
+
+EPI_BF16_LN, EPI_GELU_LN, EPI_RESID_BF16_ST, EPI_RESID_FFN_BF16_ST, EPI_POS_BF16_ST = 8, 9, 10, 11, 12
+
+
+def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln_rs=None,
+                ln_c=None, st_part=None, stream=None):
+    """bf16 w4 GEMM with a GEMM-folded LayerNorm epilogue (8, 9) or a row-statistics
+    epilogue (10..12); all tensors contiguous on the device."""
+    M, K = a.shape
+    N = w.shape[0]
+    call("vp_dev_gemm_ln", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
+         _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad), _ptr(ln_rs), _ptr(ln_c),
+         _ptr(st_part), _stream(stream))
+    return out
+
+
+def dev_ln_stats(src, M, D, out, from_partials, stream=None):
+    """(rstd, -mean*rstd) per row from partial statistics (from_partials) or bf16 rows."""
+    call("vp_dev_ln_stats", 0 if from_partials else 1, _ptr(src), M, D, _ptr(out), _stream(stream))
     return out
 
 
