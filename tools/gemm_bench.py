@@ -108,7 +108,9 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    if mode == "nt":
+    if mode == "early":
+        variants(dev, g, 4, [0, 1024, 2048, 4096])
+    elif mode == "nt":
         variants(dev, g, 4, [0, 256, 8])
     elif mode == "cmp":
         compare(dev, g)

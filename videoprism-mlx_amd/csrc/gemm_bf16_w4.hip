@@ -56,7 +56,11 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
 // K-tile, so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
 // schedule with the 16 loads and 16 reads in its first 32 MFMAs, 256 = plain (temporal) output stores.
-template <int EPI, int DIAG = 0>
+// PF > 0: L2 prefetch of A, PF K-tiles beyond the K-tile being staged (one dword per A row per
+// K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  Pays where A streams
+// from HBM (ffn_layer2, K = 3072: 490 -> 471 us); costs on the K = 768 shapes (A mostly from the
+// Infinity Cache).
+template <int EPI, int DIAG = 0, int PF = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, EpiArgs ep) {
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
 #pragma unroll
   for (int q = 0; q < 16; ++q) rd(0, 0, q);
 
-  // h0 of K-tile g (buffer cb): MFMAs set 0, reads of set 1 <- (g, h1)
+  uint32_t pf_dummy = 0;  // PF: destination of the L2-prefetch loads (never read)
   auto h0 = [&](int cb, bool zero) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     sched_fence();
@@ -189,6 +193,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   auto h1 = [&](int cb, bool after_epi) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (after_epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if constexpr (PF > 0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sched_fence();
     mfma(1, 0, false);
@@ -226,6 +231,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     }
     sched_fence();
+    if constexpr (PF > 0) {
+      // L2 prefetch of A for K-tile (load position + PF); past the row end it touches the next
+      // row (or returns 0 beyond the buffer): harmless
+      const uint32_t voff = (uint32_t)(ld_tm * BM + w * 64 + lane) * a_rb + (ld_kt + PF) * (BK * 2);
+      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "+v"(pf_dummy) : "v"(voff), "s"(rsA));
+      sched_fence();
+    }
     advance();  // after the scheduled block: its branch must not split it
   };
 
@@ -391,6 +403,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+constexpr int kPfLongK = 2;  // A prefetch distance (K-tiles) for K >= 2048
+
 int num_cus_w4() {
   static int n = 0;
   if (n == 0) {
@@ -402,19 +416,19 @@ int num_cus_w4() {
   return n;
 }
 
-template <int EPI, int DIAG = 0>
+template <int EPI, int DIAG = 0, int PF = 0>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG, PF>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
-  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
+  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
                      ldw, M, N, K, ep);
   return hipGetLastError();
 }
@@ -442,22 +456,11 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 128: return launch_w4<EPI_BF16, 128>(A, lda, W, ldw, M, N, K, ep, s);
       case 136: return launch_w4<EPI_BF16, 136>(A, lda, W, ldw, M, N, K, ep, s);
       case 256: return launch_w4<EPI_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+      case 1024: return launch_w4<EPI_BF16, 0, 2>(A, lda, W, ldw, M, N, K, ep, s);
+      case 2048: return launch_w4<EPI_BF16, 0, 3>(A, lda, W, ldw, M, N, K, ep, s);
+      case 4096: return launch_w4<EPI_BF16, 0, 4>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
-  }
-  static int nt = -1;
-  if (nt < 0) {
-    const char* e = getenv("VP_GEMM_NT");
-    nt = (e && e[0] == '0') ? 0 : 1;
-  }
-  if (!nt) {  // plain (temporal) output stores
-    switch (epi) {
-      case EPI_BF16: return launch_w4<EPI_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
-      case EPI_GELU_BF16: return launch_w4<EPI_GELU_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
-      case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
-      case EPI_POS_BF16: return launch_w4<EPI_POS_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
-      case EPI_RESID_FFN_BF16: return launch_w4<EPI_RESID_FFN_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
-    }
   }
   switch (epi) {
     case EPI_BF16: return launch_w4<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s);
@@ -467,11 +470,15 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
     case EPI_RESID_FFN: return launch_w4<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16: return launch_w4<EPI_POS_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN_BF16: return launch_w4<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16:
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_BF16_LN: return launch_w4<EPI_BF16_LN>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_GELU_BF16_LN: return launch_w4<EPI_GELU_BF16_LN>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN_BF16_ST: return launch_w4<EPI_RESID_FFN_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16_ST:
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_RESID_FFN_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;

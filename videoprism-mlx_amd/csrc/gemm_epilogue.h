@@ -145,8 +145,8 @@ __device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, 
 // v = acc + bias (8 columns); same math and single rounding as epi_store
 typedef unsigned epi_u32x4 __attribute__((ext_vector_type(4)));
 // NT: nontemporal output stores (global_store ... nt).  Measured on the w4 kernel at the
-// encoder's shapes: qkv 432 -> 379 us, post 147 -> 130 us, ffn1 579 -> 502 us (the output
-// streams past L2 instead of being written back from it later; tools/gemm_bench.py nt).
+// encoder's shapes in isolation: qkv 432 -> 379 us, post 147 -> 130 us, ffn1 579 -> 502 us
+// (tools/gemm_bench.py nt); inside the full forward within +-1 %.
 // returns the stored bf16 values (packed) for the row-statistics epilogues
 template <int EPI, bool NT = true>
 __device__ __forceinline__ epi_u32x4 epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
