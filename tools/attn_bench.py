@@ -1,0 +1,51 @@
+"""Spatial attention microbenchmark at the bench shape (B=32 clips x 16 frames = 512 sequences
+of 256 tokens, 12 heads): production kernel and its ablation builds (DIAG bits, see
+attention.hip), interleaved rounds in one process."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
+import torch  # noqa: E402
+
+from videoprism import _native as nat  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = torch.device("cuda:0")
+    nseq, heads, S = 512, 12, 256
+    g = torch.Generator(device=dev).manual_seed(0)
+    D = heads * 64
+    qkv = torch.randn((nseq * S, 3 * D), generator=g, device=dev)
+    qkv[:, :D] *= 0.125
+    qkv = qkv.to(torch.bfloat16)
+    o = torch.empty((nseq * S, D), device=dev, dtype=torch.bfloat16)
+    st = lambda: torch.cuda.current_stream().cuda_stream
+    diags = [int(a) for a in sys.argv[1:]] or [0, 1, 2, 3]
+    fns = {f"d{d}": (lambda d=d: nat.call("vp_dev_attention_diag", d, qkv.data_ptr(), o.data_ptr(), nseq,
+                                          heads, 50.0, st())) for d in diags}
+    fns["prod"] = lambda: nat.op_attention(qkv, nseq, S, heads, 50.0, out=o)
+    res = {k: [] for k in fns}
+    for _ in range(3):
+        for k, f in fns.items():
+            res[k].append(timeit(f))
+    flop = 4.0 * nseq * S * S * D
+    print("spatial attention:", " ".join(f"{k}: {min(v)*1e3:6.1f} us ({flop/min(v)/1e9:5.0f} TF)"
+                                        for k, v in res.items()), flush=True)
+
+
+if __name__ == "__main__":
+    main()

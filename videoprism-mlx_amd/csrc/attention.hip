@@ -17,6 +17,8 @@
 // attention_temporal_bf16: S = T <= 16 frames.  One wave per (sequence, head), 16x16x32 for
 //   Q.K^T and 16x16x16 for P.V; memory-bound on the qkv rows.
 // attention_f32: generic fp32 path (fprop_dtype=float32), online softmax, exact tanhf/expf.
+#include <cstdlib>
+
 #include "vp_common.h"
 #include "vp_kernels.h"
 
@@ -51,10 +53,11 @@ constexpr int kSpS = 256;
 constexpr int kSpThreads = 512;
 constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 
-template <bool MASK>
+// DIAG (ablation builds, results garbage): 1 = no capped-exp VALU (p = logit), 2 = no P.V MFMAs
+template <bool MASK, int DIAG = 0>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
-    const float* __restrict__ key_pad) {
+    const float* __restrict__ key_pad, int rev) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + kSpS * 128;
@@ -63,8 +66,11 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
 
   const int D = heads * 64;
   const int64_t ld = 3 * (int64_t)D;
-  const int seq = blockIdx.x / heads;
-  const int h = blockIdx.x % heads;
+  // rev: sequences in reverse order, so the last-written (Infinity-Cache resident) q|k|v rows
+  // of the producing GEMM are read first
+  const int bid = rev ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int seq = bid / heads;
+  const int h = bid % heads;
   const int lane = threadIdx.x & 63;
   const int w = wave_id();
   const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * 64;
@@ -126,7 +132,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     float p[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float e = capped_exp(x[i], c1, c2);
+      float e = (DIAG & 1) ? x[i] : capped_exp(x[i], c1, c2);
       if constexpr (MASK) {
         const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
         e = all_masked ? 1.0f : (kp[key] != 0.0f ? 0.0f : e);
@@ -154,10 +160,13 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
         const bf16x4 lo = tr_read(ad);
         const bf16x4 hi = tr_read(ad + 8 * 128);
         const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (dh == 0)
+        if constexpr (DIAG & 2) {
+          asm volatile("" ::"v"(vf), "v"(pf[s]));
+        } else if (dh == 0) {
           y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y0, 0, 0, 0);
-        else
+        } else {
           y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y1, 0, 0, 0);
+        }
       }
     }
   }
@@ -357,11 +366,30 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
     attr[mi] = true;
   }
   const dim3 grid(num_seq * heads);
+  const int rev = 0;  // reverse order measured no faster (the q|k|v stream is HBM-resident either way)
   if (key_pad)
-    hipLaunchKernelGGL(attn_spatial_kernel<true>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad);
+    hipLaunchKernelGGL(attn_spatial_kernel<true>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad, rev);
   else
-    hipLaunchKernelGGL(attn_spatial_kernel<false>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad);
+    hipLaunchKernelGGL(attn_spatial_kernel<false>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad, rev);
   return hipGetLastError();
+}
+
+hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
+                                  float cap, hipStream_t s) {
+  const dim3 grid(num_seq * heads);
+  auto go = [&](const void* fn, auto kern) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, nullptr, 0);
+    return hipGetLastError();
+  };
+  switch (diag) {
+    case 0: return go((const void*)attn_spatial_kernel<false, 0>, attn_spatial_kernel<false, 0>);
+    case 1: return go((const void*)attn_spatial_kernel<false, 1>, attn_spatial_kernel<false, 1>);
+    case 2: return go((const void*)attn_spatial_kernel<false, 2>, attn_spatial_kernel<false, 2>);
+    case 3: return go((const void*)attn_spatial_kernel<false, 3>, attn_spatial_kernel<false, 3>);
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,

@@ -435,6 +435,34 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
 
 }  // namespace
 
+namespace {
+// production epilogues; D = 0: nontemporal output stores, D = 256: plain stores (ablation)
+template <int D>
+hipError_t w4_dispatch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
+                       int K, const EpiArgs& ep, hipStream_t s) {
+  switch (epi) {
+    case EPI_BF16: return launch_w4<EPI_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_GELU_BF16: return launch_w4<EPI_GELU_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_F32: return launch_w4<EPI_RESID_F32, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_F32: return launch_w4<EPI_POS_F32, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN: return launch_w4<EPI_RESID_FFN, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_BF16: return launch_w4<EPI_POS_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16:
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16, D, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_RESID_FFN_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_BF16_LN: return launch_w4<EPI_BF16_LN, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_GELU_BF16_LN: return launch_w4<EPI_GELU_BF16_LN, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16_ST:
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, D, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_RESID_FFN_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
+  }
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s) {
   // byte offsets into A / W must fit the 32-bit buffer range
@@ -462,25 +490,9 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
     }
     return hipErrorInvalidValue;
   }
-  switch (epi) {
-    case EPI_BF16: return launch_w4<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_GELU_BF16: return launch_w4<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_F32: return launch_w4<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_POS_F32: return launch_w4<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN: return launch_w4<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_POS_BF16: return launch_w4<EPI_POS_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN_BF16:
-      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
-      return launch_w4<EPI_RESID_FFN_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_BF16_LN: return launch_w4<EPI_BF16_LN>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_GELU_BF16_LN: return launch_w4<EPI_GELU_BF16_LN>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN_BF16_ST:
-      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
-      return launch_w4<EPI_RESID_FFN_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST>(A, lda, W, ldw, M, N, K, ep, s);
-  }
+  // nontemporal output stores: +1.7 % on the whole forward vs plain stores (same device,
+  // back-to-back runs: 947.8 vs 931.7 clips/s)
+  return w4_dispatch<0>(epi, A, lda, W, ldw, M, N, K, ep, s);
   return hipErrorInvalidValue;
 }
 

@@ -790,6 +790,14 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
   return VP_OK;
 }
 
+// ablation builds of the spatial attention kernel (tools/attn_bench.py)
+int vp_dev_attention_diag(int diag, const void* qkv, void* o, int64_t num_seq, int64_t heads, float cap,
+                          void* stream) {
+  VP_HIP(vp::attention_spatial_diag(diag, (const vp::bf16_t*)qkv, (vp::bf16_t*)o, (int)num_seq, (int)heads, cap,
+                                    static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // which = 0: ln_stats_finalize(src = st_part [D/128][M][2]); 1: ln_row_stats(src = bf16 [M][D])
 int vp_dev_ln_stats(int which, const void* src, int64_t M, int64_t D, float* ln_rs, void* stream) {
   using namespace vp;

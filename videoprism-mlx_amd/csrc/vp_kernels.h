@@ -78,6 +78,9 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
 // o: rows of D = heads*64.  key_pad: optional [num_seq * S] (1 = padded key).
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, const float* key_pad, hipStream_t s);
+// ablation builds of the spatial kernel (tools/attn_bench.py)
+hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
+                                  float cap, hipStream_t s);
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s);
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,

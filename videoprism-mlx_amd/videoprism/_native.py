@@ -85,6 +85,7 @@ _SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "vp_dev_attention_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
 }
 
 _lib = None
