@@ -104,11 +104,37 @@ def variants(dev, g, which, diags):
               "| us:", " ".join(f"d{d}:{min(t)*1e3:6.1f}" for d, t in res.items()), flush=True)
 
 
+def folded(dev, g):
+    """The forward's LN-folded / row-statistics epilogues at the encoder shapes vs the plain ones."""
+    cases = [("qkv", 2304, 768, nat.EPI_STORE, nat.EPI_BF16_LN), ("post", 768, 768, nat.EPI_RESID_BF16, nat.EPI_RESID_BF16_ST),
+             ("ffn1", 3072, 768, nat.EPI_GELU, nat.EPI_GELU_LN), ("ffn2", 768, 3072, nat.EPI_RESID_FFN_BF16, nat.EPI_RESID_FFN_BF16_ST)]
+    for name, N, K, plain, fold in cases:
+        M = M_TOK
+        a, w, b = operands(M, N, K, g, dev)
+        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        resid = plain in (nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16)
+        rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
+        c = torch.zeros(N, device=dev)
+        part = torch.empty((N // 128, M, 2), device=dev)
+        fns = {"plain": lambda: nat.dev_gemm_kernel(4, a, w, b, plain, o, resid=o if resid else None),
+               "fold": lambda: nat.dev_gemm_ln(a, w, b, fold, o, resid=o if resid else None, ln_rs=rs, ln_c=c,
+                                               st_part=part)}
+        res = {k: [] for k in fns}
+        for _ in range(3):
+            for k, f in fns.items():
+                res[k].append(timeit(f))
+        flop = 2.0 * M * N * K
+        print(f"{name} epi {plain} vs {fold}: " + " | ".join(f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF"
+                                                          for k, v in res.items()), flush=True)
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    if mode == "early":
+    if mode == "fold":
+        folded(dev, g)
+    elif mode == "early":
         variants(dev, g, 4, [0, 1024, 2048, 4096])
     elif mode == "nt":
         variants(dev, g, 4, [0, 256, 8])
