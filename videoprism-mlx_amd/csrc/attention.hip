@@ -18,6 +18,7 @@
 //   Q.K^T and 16x16x16 for P.V; memory-bound on the qkv rows.
 // attention_f32: generic fp32 path (fprop_dtype=float32), online softmax, exact tanhf/expf.
 #include <cstdlib>
+#include <type_traits>
 
 #include "vp_common.h"
 #include "vp_kernels.h"
@@ -75,31 +76,52 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   const int w = wave_id();
   const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * 64;
 
-  // ---- stage K (pieces 0..31) and V (32..63): 8 pieces of 8 rows x 128 B per wave ----
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int piece = w * 8 + i;
-    const bool isV = piece >= 32;
-    const int row = (piece & 31) * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
-    const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * D : D) + c * 8;
-    __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
-  }
-  // ---- this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j) ----
+  // ---- this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j),
+  // requested first by loads the compiler does not see (a visible load would make hipcc wait
+  // vmcnt(0) at its first use and drain the K/V stream below); retired by the chunk-0 wait ----
   const int q0 = w * 32;
   const int half = lane >> 5;
   bf16x8 qf[4];
   {
     const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
 #pragma unroll
-    for (int kd = 0; kd < 4; ++kd) qf[kd] = *reinterpret_cast<const bf16x8*>(qp + 16 * kd);
+    for (int kd = 0; kd < 4; ++kd)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qp + 16 * kd));
   }
-  if constexpr (MASK) {
+  // ---- stage K and V in 4 chunks of 64 keys, chunk-major: wave w loads K piece c*8+w and
+  // V piece 32+c*8+w of chunk c (a piece = 8 keys x 128 B), so key tiles 2c, 2c+1 can start as
+  // soon as chunk c has landed while the later chunks are still in flight ----
+#pragma unroll
+  for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+    for (int isV = 0; isV < 2; ++isV) {
+      const int piece = isV * 32 + cc * 8 + w;
+      const int row = (piece & 31) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
+      const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * D : D) + c * 8;
+      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
+    }
+  if constexpr (MASK) {  // (padded batches: no streaming)
     if (threadIdx.x < kSpS) kp[threadIdx.x] = key_pad[(int64_t)seq * kSpS + threadIdx.x];
     if (threadIdx.x == 0) *allmask = 1;
+    wait_vmcnt0();
+    __syncthreads();
   }
-  wait_vmcnt0();
-  __syncthreads();
+  // chunk cc of every wave has landed: this wave's vmcnt leaves only its younger chunks in
+  // flight, then one barrier
+  auto chunk_ready = [&](auto CC) {
+    constexpr int cc = decltype(CC)::value;
+    if constexpr (!MASK) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (3 - cc)) : "memory");
+      if constexpr (cc == 0) {
+#pragma unroll
+        for (int kd = 0; kd < 4; ++kd) asm volatile("" : "+v"(qf[kd]));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   bool all_masked = false;
   if constexpr (MASK) {
     if (threadIdx.x < kSpS && kp[threadIdx.x] == 0.0f) *allmask = 0;
@@ -116,8 +138,14 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   const int li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
 
+  chunk_ready(std::integral_constant<int, 0>{});
+#pragma unroll 1
+  for (int cc = 0; cc < 4; ++cc) {
+  if (cc == 1) chunk_ready(std::integral_constant<int, 1>{});
+  else if (cc == 2) chunk_ready(std::integral_constant<int, 2>{});
+  else if (cc == 3) chunk_ready(std::integral_constant<int, 3>{});
 #pragma unroll 2
-  for (int kt = 0; kt < kSpS / 32; ++kt) {
+  for (int kt = 2 * cc; kt < 2 * cc + 2; ++kt) {
     // S^T tile: X[key][q], keys kt*32 .. +31
     f32x16 x = {};
     const int krow = kt * 32 + krow_l;
@@ -148,7 +176,10 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       for (int j = 0; j < 4; ++j) u[j] = pack_bf16x2(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
       pf[s] = *reinterpret_cast<bf16x8*>(u);
     }
-    // O^T += V^T . X  (A = V^T via transposed reads, B = P^T numerators)
+    // O^T += V^T . X  (A = V^T via transposed reads, B = P^T numerators).  The transposed reads
+    // are inline asm: hipcc puts a vmcnt(0) for the in-flight K/V chunks in front of a visible
+    // ds_read_tr (it cannot tell it from a read of a chunk still landing); lgkmcnt(0) retires them
+    s16x4 vr[2][2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int key = kt * 32 + 16 * s + 4 * half + trq;
@@ -156,9 +187,24 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       for (int dh = 0; dh < 2; ++dh) {
         const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
         const int c = col >> 3;
-        const char* ad = Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2;
-        const bf16x4 lo = tr_read(ad);
-        const bf16x4 hi = tr_read(ad + 8 * 128);
+        const uint32_t ad = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2);
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[s][dh][0]) : "v"(ad));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(vr[s][dh][1]) : "v"(ad));
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        asm volatile("" : "+v"(vr[s][dh][0]), "+v"(vr[s][dh][1]));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const s16x4 lo = vr[s][dh][0], hi = vr[s][dh][1];
         const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         if constexpr (DIAG & 2) {
           asm volatile("" ::"v"(vf), "v"(pf[s]));
@@ -169,6 +215,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
         }
       }
     }
+  }
   }
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;
