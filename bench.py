@@ -85,7 +85,7 @@ def main() -> None:
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01_v4.json"))
     args = ap.parse_args()
 
     import torch

@@ -27,7 +27,7 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
         dur[k].append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-9)
 for k, cs in vals.items():
-    if not (k.startswith("gemm") or k.startswith("hipblas") or "attn" in k or "layernorm" in k):
+    if not (k.startswith("gemm") or k.startswith("hipblas") or "attn" in k or "layernorm" in k or "ln_" in k):
         continue
     m = {c: sum(v) / len(v) for c, v in cs.items()}
     t = sum(dur[k]) / len(dur[k])
@@ -48,13 +48,13 @@ for k, cs in vals.items():
 
 # --json OUT: per-launch HBM bytes of the bench's kernel classes (bench.py reads it for the
 # roofline's `traffic`): 2 x FETCH_SIZE (gfx950 rule) + WRITE_SIZE, KiB counters.
-CLASS_OF = {  # kernel instance -> vp_profile class (vp_abi.cpp kProfNames)
-    "gemm_bf16_w4_kernel<1, 0>": "gemm_ffn1_gelu",
-    "gemm_bf16_w4_kernel<7, 0>": "gemm_ffn2",
-    "gemm_bf16_w4_kernel<0, 0>": "gemm_qkv",
-    "gemm_bf16_w4_kernel<5, 0>": "gemm_post",
-    "gemm_bf16_w4_kernel<6, 0>": "gemm_patch_embed",
-    "attn_spatial_kernel<false>": "attention_spatial",
+CLASS_OF = {  # kernel instance -> vp_profile class (vp_abi.cpp kProfNames); <EPI, DIAG, PF>
+    "gemm_bf16_w4_kernel<9, 0, 0>": "gemm_ffn1_gelu",      # EPI_GELU_BF16_LN
+    "gemm_bf16_w4_kernel<11, 0, 2>": "gemm_ffn2",          # EPI_RESID_FFN_BF16_ST, A prefetch
+    "gemm_bf16_w4_kernel<8, 0, 0>": "gemm_qkv",            # EPI_BF16_LN
+    "gemm_bf16_w4_kernel<10, 0, 0>": "gemm_post",          # EPI_RESID_BF16_ST
+    "gemm_bf16_w4_kernel<12, 0, 0>": "gemm_patch_embed",   # EPI_POS_BF16_ST
+    "attn_spatial_kernel<false, 0>": "attention_spatial",
     "attn_temporal_kernel<false>": "attention_temporal",
 }
 if len(sys.argv) > 3 and sys.argv[2] == "--json":
