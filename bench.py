@@ -45,6 +45,32 @@ def gflop_per_clip(cfg: dict, T: int = 16, N: int = 256) -> float:
     return (gemm + sp_att + tp_att + patch) / 1e9
 
 
+def lvt_gflop_per_clip(cfg: dict, T: int = 16, N: int = 256) -> float:
+    """LvT video side: vision encoder + auxiliary encoder (GEMMs + attention over all T*N tokens)
+    + the pooler FLOPs this build executes (logits and weighted sum, 4*tok*D*heads; the
+    reference's K/V projections of the tokens, 16*tok*D^2, are eliminated algebraically)."""
+    D, F, La = cfg["model_dim"], cfg["mlp_dim"], cfg["num_auxiliary_layers"]
+    tok = T * N
+    aux = (8 * D * D + 4 * D * F) * tok * La + 4 * tok * tok * D * La
+    pool = 4 * tok * D * cfg["num_heads"]
+    return gflop_per_clip(cfg, T, N) + (aux + pool) / 1e9
+
+
+def text_gflop_per_query(cfg: dict, L: int = 64) -> float:
+    D = cfg["model_dim"]
+    tok = L + 1
+    return ((8 * D * D + 16 * D * D) * tok + 4 * tok * tok * D) * cfg["num_unimodal_layers"] / 1e9
+
+
+WORKLOADS = {
+    # name: (model name, CONFIGS key, default clips per GPU)
+    "base": ("videoprism_public_v1_base", "videoprism_v1_base", 32),          # configs[1]/[3]
+    "large": ("videoprism_public_v1_large", "videoprism_v1_large", 16),       # configs[2]
+    "lvt_large": ("videoprism_lvt_public_v1_large", "videoprism_lvt_v1_large", 32),  # configs[4]
+    "lvt_base": ("videoprism_lvt_public_v1_base", "videoprism_lvt_v1_base", 32),
+}
+
+
 def cpu_baseline(cfg, variables) -> dict:
     """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip — a reported baseline only."""
     import numpy as np
@@ -80,7 +106,11 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--workload", default="base", choices=sorted(WORKLOADS),
+                    help="base = configs[1] (default, the headline metric); large = configs[2]; "
+                         "lvt_large = configs[4] video+text")
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU")
+    ap.add_argument("--queries", type=int, default=8, help="text queries (LvT workloads)")
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,28 +128,52 @@ def main() -> None:
     torch.cuda.set_device(local_rank)
     dev = torch.device(f"cuda:{local_rank}")
 
-    name = "videoprism_public_v1_base"
-    cfg = models.CONFIGS["videoprism_v1_base"]
-    variables = params.synthetic_params(cfg, seed=0)
+    name, cfg_key, default_b = WORKLOADS[args.workload]
+    lvt = args.workload.startswith("lvt")
+    cfg = dict(models.CONFIGS[cfg_key])
     model = models.get_model(name, fprop_dtype=torch.bfloat16)
+    if lvt:
+        cfg["vocabulary_size"] = model.vocabulary_size
+        variables = params.synthetic_params(cfg, seed=0, specs=params.clip_leaf_specs(cfg))
+    else:
+        variables = params.synthetic_params(cfg, seed=0)
     eng = model.engine(variables, local_rank)
 
-    B, T = args.batch, args.frames
+    B, T = args.batch or default_b, args.frames
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev).to(torch.bfloat16)
-    out = torch.empty((B, T * 256, cfg["model_dim"]), dtype=torch.bfloat16, device=dev)
     gather = world > 1 and not args.no_allgather
+    if lvt:
+        # configs[4]: text ids randint(0, V) [Q, 64] with the second half of every other query
+        # padded (models_test.py:61-69), replicated on every rank
+        Q, Lt = args.queries, 64
+        tgen = torch.Generator(device=dev).manual_seed(7)
+        ids = torch.randint(0, cfg["vocabulary_size"], (Q, Lt), generator=tgen, device=dev,
+                            dtype=torch.int32)
+        tpad = torch.zeros((Q, Lt), dtype=torch.float32, device=dev)
+        tpad[1::2, Lt // 2:] = 1.0
 
-    def step():
-        eng.forward(video, out=out)
-        if gather:
-            pooled = _native.op_pool_l2(out)
-            distributed.all_gather_rows(pooled, world)
+        def step():
+            vemb = eng.encode_video(video)[0]
+            if gather:
+                vemb = distributed.all_gather_rows(vemb, world)
+            temb = eng.encode_text(ids, tpad)
+            _native.op_similarity(vemb, temb)
+    else:
+        out = torch.empty((B, T * 256, cfg["model_dim"]), dtype=torch.bfloat16, device=dev)
+
+        def step():
+            eng.forward(video, out=out)
+            if gather:
+                pooled = _native.op_pool_l2(out)
+                distributed.all_gather_rows(pooled, world)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     launches_per_fwd = 3 + 7 * (cfg["num_spatial_layers"] + cfg["num_temporal_layers"]) + 2
+    if lvt:
+        launches_per_fwd += 8 * cfg["num_auxiliary_layers"] + 4 + 8 * cfg["num_unimodal_layers"] + 8
     if not args.no_profile:
         eng.profile_enable(args.steps * launches_per_fwd + 16)
     distributed.barrier(dev)
@@ -135,7 +189,8 @@ def main() -> None:
     clips = world * B * args.steps
     value = clips / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    gpc = gflop_per_clip(cfg, T)
+    gpc = lvt_gflop_per_clip(cfg, T) if lvt else gflop_per_clip(cfg, T)
+    text_gf = text_gflop_per_query(cfg) * args.queries if lvt else 0.0
 
     roofline = None
     kernel_ms = {}
@@ -160,23 +215,29 @@ def main() -> None:
                          else dom["bytes"] / dom["launches"], "traffic_source": tsrc})
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not lvt:
         cpu = cpu_baseline(cfg, variables)
 
     if rank == 0:
+        label = {"base": "VideoPrism-Base fwd", "large": "VideoPrism-Large fwd",
+                 "lvt_large": "VideoPrism-LvT-Large video+text fwd",
+                 "lvt_base": "VideoPrism-LvT-Base video+text fwd"}[args.workload]
+        wl = (f"{name} bf16 forward, B={B} clips/GPU x {world} GPU, {T}x288x288x3"
+              + (f", {args.queries} text queries x 64 tokens, gathered video_emb @ text_emb.T"
+                 if lvt else "")
+              + (", RCCL all-gather of pooled embeddings" if gather else ""))
         line = {
-            "metric": "clips/sec (16x288x288) VideoPrism-Base fwd; % MFMA peak",
+            "metric": f"clips/sec (16x288x288) {label}; % MFMA peak",
             "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic uniform[0,1) clips generated on device; random-init weights of the "
                     "real architecture (no checkpoint offline)",
-            "config": {"workload": f"{name} bf16 forward, B={B} clips/GPU x {world} GPU, "
-                                   f"{T}x288x288x3" + (", RCCL all-gather of pooled embeddings"
-                                                       if gather else ""),
+            "config": {"workload": wl,
                        "model": name, "global_batch": B * world, "frames": T,
                        "parallelism": f"dp{world} (batch-sharded clips)"},
-            "mfma_util_whole_forward": round(value / world * gpc / 1e3 / PEAK_BF16_TFLOPS, 4),
+            "mfma_util_whole_forward": round((value / world * gpc + text_gf / ms_per_step * 1e3)
+                                             / 1e3 / PEAK_BF16_TFLOPS, 4),
             "gflop_per_clip": round(gpc, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VP_ABI_VERSION 2
+#define VP_ABI_VERSION 3
 
 typedef struct vp_handle vp_handle;
 
@@ -125,7 +125,8 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
 
 /* Capped attention over rows qkv[num_seq*S, 3*heads*64] = [q|k|v] (q pre-scaled), writing
  * o[num_seq*S, heads*64].  Replaces DotProductAttention._dot_atten (layers.py:601-661).
- * precision VP_BF16 (S == 256 or S <= 16) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL. */
+ * precision VP_BF16 (S == 256 or S <= 16; S a multiple of 256 without key_pad: the long-sequence
+ * kernel of the LvT auxiliary encoder) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL. */
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
                     int64_t heads, float cap, const float* key_pad, void* stream);
 
@@ -145,6 +146,70 @@ int vp_op_patchify(const void* video, int in_dtype, void* patches, int out_dtype
  * reference's _l2_normalize (encoders.py:50-67, eps 1e-12). */
 int vp_op_pool_l2(const void* emb, int dtype, int64_t B, int64_t L, int64_t D, float* out,
                   void* stream);
+
+/* Generic fp32-math attention over rows qkv[num_seq*S, 3*heads*64] (q pre-scaled), any S, with
+ * key paddings key_pad [num_seq*S] (nullable) and, if causal, the merged causal + padding mask of
+ * layers.py:111-179 (a padded query row is fully masked -> uniform weights).  qkv / o in
+ * `precision` (VP_F32 or VP_BF16).  cap <= 0 disables the tanh cap.  Used by the text tower. */
+int vp_op_attention_masked(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
+                           int64_t heads, float cap, const float* key_pad, int causal, void* stream);
+
+/* video_emb [B, D] . text_emb [Q, D]^T -> out [B, Q] (fp32): the video-text similarity of the
+ * LvT models (README / colab usage of FactorizedVideoCLIP's embeddings). */
+int vp_op_similarity(const float* video_emb, const float* text_emb, int64_t B, int64_t Q, int64_t D,
+                     float* out, void* stream);
+
+/* ---------------- LvT video-text model: FactorizedVideoCLIP (encoders.py:762-910) ----------------
+ * Replaces models.get_model('videoprism_lvt_public_v1_{base,large}') + model.apply(variables,
+ * inputs, text_token_ids, text_paddings, train=False, normalize, return_intermediate,
+ * frame_paddings) (models.py:116-212, 268-303).  Parameters are the Flax leaves under 'params':
+ * 'vision_encoder/...' (the FactorizedEncoder leaves above), 'auxiliary_encoder/...',
+ * 'contrastive_vision_pooler/...', 'text_encoder/...' (88 leaves for a scanned model,
+ * encoders_test.py:339).  Same conventions as vp_handle (borrowed device pointers, async on
+ * `stream`, no allocation in the encode calls, one device per handle, not thread-safe). */
+typedef struct vp_clip vp_clip;
+
+typedef struct vp_clip_config {
+  vp_config video;               /* vision encoder hyper-parameters (models.py:116-145) */
+  int32_t num_auxiliary_layers;  /* 2: VisionTransformer over all T*N tokens (:846-857) */
+  int32_t vocabulary_size;       /* 32000 (c4_en, models.py:55-60) */
+  int32_t num_unimodal_layers;   /* 12: text tower depth */
+  int32_t enable_causal_atten;   /* 1 */
+} vp_clip_config;
+
+int vp_clip_create(const vp_clip_config* cfg, int device, vp_clip** out);
+int vp_clip_destroy(vp_clip* c);
+int vp_clip_set_param(vp_clip* c, const char* name, const float* host_data, const int64_t* shape,
+                      int ndim);
+int vp_clip_param_count(const vp_clip* c, int* count);
+int vp_clip_param_name(const vp_clip* c, int index, const char** name);
+int vp_clip_finalize(vp_clip* c);
+/* The vision tower's vp_handle (owned by the clip): vp_profile_* on it also covers the
+ * auxiliary encoder and pooler launches of vp_clip_encode_video. */
+int vp_clip_video_handle(vp_clip* c, vp_handle** video);
+
+/* Video side of FactorizedVideoCLIP.__call__ (encoders.py:833-885):
+ *   video_emb      device [B, D] fp32: contrastive_vision_pooler(auxiliary_encoder(features)),
+ *                  L2-normalised if `normalize` (:859-872)
+ *   frame_emb      device [B, T, D] fp32 'frame_embeddings' (pooler per frame, :874-885) or NULL
+ *   spatial_out    device [B, T*N, D] 'spatial_features' in out_dtype, or NULL
+ *   spatiotemporal_out device [B, T*N, D] 'spatiotemporal_features' (the vision encoder's output,
+ *                  :844-845) in the handle's fprop dtype (out_dtype must match), or NULL */
+int vp_clip_video_workspace_bytes(const vp_clip* c, int64_t B, int64_t T, int64_t H, int64_t W,
+                                  size_t* bytes);
+int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B, int64_t T,
+                         int64_t H, int64_t W, const float* frame_paddings, int normalize,
+                         float* video_emb, float* frame_emb, void* spatial_out,
+                         void* spatiotemporal_out, int out_dtype, void* workspace,
+                         size_t ws_bytes, void* stream);
+
+/* Text side (encoders.py:887-908): ids device int32 [Q, L], paddings device fp32 [Q, L]
+ * (1 = padded token); text_emb device [Q, D] fp32 = the CLS token after unimodal_ln,
+ * L2-normalised if `normalize`.  Out-of-range ids are clamped (JAX gather semantics). */
+int vp_clip_text_workspace_bytes(const vp_clip* c, int64_t Q, int64_t L, size_t* bytes);
+int vp_clip_encode_text(vp_clip* c, const int32_t* ids, const float* paddings, int64_t Q,
+                        int64_t L, int normalize, float* text_emb, void* workspace,
+                        size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

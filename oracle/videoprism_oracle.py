@@ -22,6 +22,14 @@ rounding emulation), the Flax reference at /root/reference/videoprism:
   * encoders.py:269-307     TrainablePositionalEmbedding (slice of emb_var)
   * encoders.py:310-388     VisionTransformer
   * encoders.py:391-580     FactorizedEncoder.__call__ / encode_with_patches
+  LvT video-text:
+  * layers.py:92-179        causal mask, _merge_masks, compute_attention_masks_for_fprop
+  * layers.py:502-527       PerDimScale (1.442695041/sqrt(dh) * softplus)
+  * layers.py:1044-1136     AttenTokenPoolingLayer
+  * encoders.py:50-67       _l2_normalize
+  * encoders.py:168-266     Embedding (index, scale_sqrt_depth), PositionalEmbedding
+  * encoders.py:656-759     TextEncoder (causal, ReLU, CLS token, unimodal_ln)
+  * encoders.py:762-910     FactorizedVideoCLIP.__call__ (auxiliary encoder, pooler, L2)
 
 PARITY UNPINNED: the reference's own tests pin only shapes and parameter-leaf
 counts (encoders_test.py:170, models_test.py:52); JAX/Flax are not installed in
@@ -159,27 +167,7 @@ def transformer_layer(x, p, paddings, mask, nm: Numerics, num_heads: int, cap: f
 
     `p` is the per-layer slice of the scanned 'x_layers' subtree.
     """
-    d = x.shape[-1]
-    h = layer_norm(x, p["layer_norm"]["scale"], p["layer_norm"]["bias"], nm)
-    sa = p["self_attention"]
-    q = attention_projection_in(h, sa["query"]["w"], sa["query"]["b"], nm)
-    k = attention_projection_in(h, sa["key"]["w"], sa["key"]["b"], nm)
-    v = attention_projection_in(h, sa["value"]["w"], sa["value"]["b"], nm)
-    enc = dot_atten(q, k, v, mask, nm, cap, d // num_heads)
-    att = attention_projection_out(enc, sa["post"]["w"], sa["post"]["b"], nm)
-    x = nm.act(att + x)                                     # :855
-    # TransformerFeedForward layers.py:370-430
-    ff = p["ff_layer"]
-    y = layer_norm(x, ff["layer_norm"]["scale"], ff["layer_norm"]["bias"], nm)
-    a = nm.act(gelu(dense(y, ff["ffn_layer1"]["linear"]["kernel"],
-                          ff["ffn_layer1"]["linear"]["bias"], nm)))
-    pad = None if paddings is None else nm.act(1.0 - paddings[..., None])
-    if pad is not None:
-        a = nm.act(a * pad)
-    o = dense(a, ff["ffn_layer2"]["linear"]["kernel"], ff["ffn_layer2"]["linear"]["bias"], nm)
-    if pad is not None:
-        o = nm.act(o * pad)
-    return nm.act(x + o)
+    return transformer_layer_act(x, p, paddings, mask, nm, num_heads, cap, gelu)
 
 
 def _layer_slice(tree, i):
@@ -348,3 +336,218 @@ def capped_softmax_attention(q, k, v, cap: float, key_mask=None):
     if key_mask is not None:
         logits = apply_mask_to_logits(logits, padding_mask(key_mask)[:, 0])
     return np.matmul(softmax(logits), v)
+
+
+# --------------------------------------------------------------------------- #
+# LvT video-text model (FactorizedVideoCLIP) — SURVEY.md §8(f) f1
+# --------------------------------------------------------------------------- #
+def relu(x):
+    """jax.nn.relu — the text tower's activation (encoders.py:743, layers.py:34)."""
+    return np.maximum(x, 0.0)
+
+
+def causal_mask(t: int):
+    """layers.py:92-108 — [1, 1, T, T], (row < col) * (-0.7*finfo.max)."""
+    row = np.arange(t)[:, None]
+    col = np.arange(t)[None, :]
+    return ((row < col).astype(np.float64) * (-0.7 * F32_MAX))[None, None]
+
+
+def merge_masks(a, b):
+    """layers.py:111-152 — elementwise minimum; a [B,1,1,S] key mask is first expanded to
+    [B,1,S,S] as min(query_mask, key_mask), so padded *queries* are fully masked too."""
+    def expand_t(key_mask):
+        return np.minimum(np.swapaxes(key_mask, -1, -2), key_mask)
+    if a.shape[-2] != b.shape[-2]:
+        if a.shape[-2] == 1:
+            a = expand_t(a)
+        else:
+            b = expand_t(b)
+    return np.minimum(a, b)
+
+
+def attention_masks_for_fprop(paddings, causal: bool):
+    """layers.py:155-179 compute_attention_masks_for_fprop."""
+    mask = padding_mask(paddings)
+    if causal:
+        mask = merge_masks(mask, causal_mask(paddings.shape[-1]))
+    return mask
+
+
+def transformer_layer_act(x, p, paddings, mask, nm: Numerics, num_heads: int, cap: float,
+                          activation=gelu):
+    """transformer_layer with a configurable FFN activation (layers.py:316-430: GELU in the
+    vision stacks, ReLU in the text tower)."""
+    d = x.shape[-1]
+    h = layer_norm(x, p["layer_norm"]["scale"], p["layer_norm"]["bias"], nm)
+    sa = p["self_attention"]
+    q = attention_projection_in(h, sa["query"]["w"], sa["query"]["b"], nm)
+    k = attention_projection_in(h, sa["key"]["w"], sa["key"]["b"], nm)
+    v = attention_projection_in(h, sa["value"]["w"], sa["value"]["b"], nm)
+    enc = dot_atten(q, k, v, mask, nm, cap, d // num_heads)
+    att = attention_projection_out(enc, sa["post"]["w"], sa["post"]["b"], nm)
+    x = nm.act(att + x)
+    ff = p["ff_layer"]
+    y = layer_norm(x, ff["layer_norm"]["scale"], ff["layer_norm"]["bias"], nm)
+    a = nm.act(activation(dense(y, ff["ffn_layer1"]["linear"]["kernel"],
+                                ff["ffn_layer1"]["linear"]["bias"], nm)))
+    pad = None if paddings is None else nm.act(1.0 - paddings[..., None])
+    if pad is not None:
+        a = nm.act(a * pad)
+    o = dense(a, ff["ffn_layer2"]["linear"]["kernel"], ff["ffn_layer2"]["linear"]["bias"], nm)
+    if pad is not None:
+        o = nm.act(o * pad)
+    return nm.act(x + o)
+
+
+def stacked_transformer_causal(x, paddings, stack, nm: Numerics, num_layers: int,
+                               num_heads: int, cap: float, causal: bool, activation=gelu):
+    """layers.py:990-1041 with enable_causal_atten and activation_fn (text tower)."""
+    if paddings is None:
+        paddings = np.zeros(x.shape[:-1])
+    mask = attention_masks_for_fprop(np.asarray(paddings, np.float64), causal)
+    if not causal and not np.any(paddings):
+        mask = None
+    xl = stack["x_layers"]
+    for i in range(num_layers):
+        x = transformer_layer_act(x, _layer_slice(xl, i), paddings, mask, nm, num_heads, cap,
+                                  activation)
+    return x
+
+
+def softplus(x):
+    return np.logaddexp(0.0, x)
+
+
+def atten_token_pooling(tokens, p, nm: Numerics, num_heads: int, hidden_dim: int):
+    """layers.py:1044-1136 AttenTokenPoolingLayer(num_queries=1, add_layer_norm=True,
+    per-dim scale on, no logit cap, paddings None) -> [B, 1, D].
+
+    q = query param projected to [N, dh] (dh = hidden_dim / N) and scaled by
+    1.442695041/sqrt(dh) * softplus(per_dim_scale) (layers.py:502-527); K, V projections of
+    the tokens; fp32 softmax (layers.py:650-654); 'post' back to D; LayerNorm.
+    """
+    b = tokens.shape[0]
+    pa = p["pooling_attention"]
+    dh = hidden_dim // num_heads
+    query = np.tile(nm.param(p["pooling_attention_query"])[None], (b, 1, 1))   # [B,1,D]
+    q = attention_projection_in(query, pa["query"]["w"], pa["query"]["b"], nm)  # [B,1,N,dh]
+    k = attention_projection_in(tokens, pa["key"]["w"], pa["key"]["b"], nm)
+    v = attention_projection_in(tokens, pa["value"]["w"], pa["value"]["b"], nm)
+    scale = nm.act(nm.act(1.442695041 / np.sqrt(dh)) *
+                   nm.act(softplus(nm.param(pa["per_dim_scale"]["per_dim_scale"]))))
+    q = nm.act(q * scale)
+    qt = np.transpose(q, (0, 2, 1, 3))
+    kt = np.transpose(k, (0, 2, 3, 1))
+    logits = nm.act(np.matmul(qt, kt))
+    sm_dt = np.float64 if nm.mode == "f64" else np.float32
+    probs = nm.act(softmax(logits.astype(sm_dt)))
+    enc = nm.act(np.matmul(probs, np.transpose(v, (0, 2, 1, 3))))
+    enc = np.transpose(enc, (0, 2, 1, 3))                                       # [B,1,N,dh]
+    out = attention_projection_out(enc, pa["post"]["w"], pa["post"]["b"], nm)   # [B,1,D]
+    ln = p["pooling_attention_layer_norm"]
+    return layer_norm(out, ln["scale"], ln["bias"], nm)
+
+
+def l2_normalize(x, eps: float = 1e-12):
+    """encoders.py:50-67 — always in fp32 (fp64 here), x / sqrt(sum x^2 + eps)."""
+    x = np.asarray(x, dtype=np.float64)
+    return x / np.sqrt(np.sum(x * x, axis=-1, keepdims=True) + eps)
+
+
+def sinusoidal_positions(seq_length: int, dim: int, min_timescale: float = 1.0,
+                         max_timescale: float = 10_000.0):
+    """encoders.py:190-224 PositionalEmbedding: [seq_length, dim] = [sin | cos] (+zero pad
+    for odd dim), computed in fp32 by the reference (restated in fp64)."""
+    position = np.arange(seq_length, dtype=np.float64)[:, None]
+    num_ts = dim // 2
+    log_inc = np.log(float(max_timescale) / float(min_timescale)) / max(num_ts - 1, 1)
+    inv = min_timescale * np.exp(np.arange(num_ts, dtype=np.float64) * -log_inc)
+    st = position * inv[None, :]
+    emb = np.concatenate([np.sin(st), np.cos(st)], axis=-1)
+    if dim % 2:
+        emb = np.pad(emb, [[0, 0], [0, 1]])
+    return emb
+
+
+def text_encoder(params, ids, paddings, cfg: dict, nm: Numerics):
+    """encoders.py:656-759 TextEncoder(num_class_tokens=1, causal, ReLU, per-dim scale off,
+    cap) -> features [B, L+1, D] after unimodal_ln.  Embedding lookup 'index' style with
+    scale_sqrt_depth (encoders.py:226-266); ids outside [0, V) clamp (JAX gather)."""
+    D = cfg["model_dim"]
+    ids = np.asarray(ids)
+    b, n = ids.shape
+    table = nm.param(params["token_emb"]["emb_var"])
+    emb = table[np.clip(ids, 0, table.shape[0] - 1)]
+    emb = nm.act(emb * nm.act(D ** 0.5))
+    pos = nm.act(sinusoidal_positions(n, D))[None]
+    feats = nm.act(emb + pos)
+    cls = np.tile(nm.param(params["cls_emb"]), (b, 1, 1))
+    cls = nm.act(cls * nm.act(D ** 0.5))
+    feats = np.concatenate([feats, cls], axis=1)
+    pad = np.concatenate([np.asarray(paddings, np.float64), np.zeros((b, 1))], axis=-1)
+    feats = stacked_transformer_causal(feats, pad, params["unimodal_transformer"], nm,
+                                       cfg["num_unimodal_layers"], cfg["num_heads"],
+                                       cfg.get("atten_logit_cap", 0.0),
+                                       cfg.get("enable_causal_atten", True), relu)
+    ln = params["unimodal_ln"]
+    return layer_norm(feats, ln["scale"], ln["bias"], nm)
+
+
+def video_clip(params, cfg: dict, inputs=None, text_token_ids=None, text_paddings=None,
+               mode: str = "f64", normalize: bool = True, return_intermediate=False,
+               frame_paddings=None):
+    """encoders.py:762-910 FactorizedVideoCLIP.__call__ -> (video_emb [B,D] | None,
+    text_emb [B,D] | None, outputs).  `params` is the tree under 'params'; cfg a CONFIGS
+    'videoprism_lvt_*' entry (models.py:116-160) plus vocabulary_size."""
+    nm = Numerics(mode)
+    D = cfg["model_dim"]
+    heads = cfg["num_heads"]
+    cap = cfg.get("atten_logit_cap", 0.0)
+    video_emb = text_emb = None
+    outputs = {}
+    if inputs is not None:
+        t = inputs.shape[-4]
+        vcfg = {k: cfg[k] for k in ("patch_size", "pos_emb_shape", "model_dim", "num_spatial_layers",
+                                    "num_temporal_layers", "num_heads", "mlp_dim",
+                                    "atten_logit_cap")}
+        feats, vout = factorized_encoder(params["vision_encoder"], inputs, vcfg, mode,
+                                         frame_paddings, return_intermediate)
+        outputs.update(vout)
+        if _contains(return_intermediate, "spatiotemporal_features"):
+            outputs["spatiotemporal_features"] = feats
+        if cfg.get("num_auxiliary_layers", 0) > 0:
+            feats = stacked_transformer_causal(
+                feats, None, params["auxiliary_encoder"]["transformers_stack"], nm,
+                cfg["num_auxiliary_layers"], heads, cap, False, gelu)       # :846-857
+        pooler = params["contrastive_vision_pooler"]
+        video_emb = atten_token_pooling(feats, pooler, nm, heads, 4 * D)[:, 0]
+        if normalize:
+            video_emb = l2_normalize(video_emb)
+        if _contains(return_intermediate, "frame_embeddings"):
+            b = feats.shape[0]
+            n = feats.shape[1] // t
+            ff = feats.reshape(b * t, n, D)                                  # :876
+            fe = atten_token_pooling(ff, pooler, nm, heads, 4 * D)[:, 0].reshape(b, t, D)
+            if normalize:
+                fe = l2_normalize(fe)
+            outputs["frame_embeddings"] = fe
+    if text_token_ids is not None:
+        assert text_paddings is not None, "Text paddings are required."
+        tf = text_encoder(params["text_encoder"], text_token_ids, text_paddings, cfg, nm)
+        text_emb = tf[:, -1]                                                 # :906
+        if normalize:
+            text_emb = l2_normalize(text_emb)
+    return video_emb, text_emb, outputs
+
+
+def masked_attention(q, k, v, cap: float, key_pad=None, causal: bool = False):
+    """Op-level restatement for the generic masked attention kernel: q,k,v [P, S, dh] with q
+    already scaled; mask = compute_attention_masks_for_fprop(key_pad, causal) (layers.py:155-179)
+    applied as in _dot_atten (layers.py:643-661).  Returns [P, S, dh]."""
+    logits = np.matmul(q, np.swapaxes(k, -1, -2))
+    if cap > 0:
+        logits = cap * np.tanh(logits / cap)
+    pad = np.zeros(q.shape[:2]) if key_pad is None else np.asarray(key_pad, np.float64)
+    mask = attention_masks_for_fprop(pad, causal)[:, 0]
+    return np.matmul(softmax(apply_mask_to_logits(logits, mask)), v)

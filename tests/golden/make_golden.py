@@ -76,10 +76,34 @@ def g4_ops():
         resize_up_8_16=orc._resize_weights(8, 16), resize_down_16_4=orc._resize_weights(16, 4))
 
 
+# encoders_test.py:290-324 — the reference's own tiny FactorizedVideoCLIP
+CLIP_TINY = dict(patch_size=4, pos_emb_shape=(16, 16, 16), num_spatial_layers=2, num_temporal_layers=2,
+                 mlp_dim=4, num_auxiliary_layers=1, vocabulary_size=20, enable_causal_atten=True,
+                 num_unimodal_layers=2, model_dim=8, num_heads=2, atten_logit_cap=50.0)
+
+
+def g5_clip_tiny():
+    cfg = CLIP_TINY
+    var = params.synthetic_params(cfg, seed=5, specs=params.clip_leaf_specs(cfg))
+    flat = params.flatten(var["params"])
+    rng = np.random.default_rng(5)
+    x = rng.normal(0.0, 0.1, (1, 4, 16, 16, 3)).astype(np.float32)
+    ids = rng.integers(0, 20, (1, 10)).astype(np.int32)
+    pads = np.zeros((1, 10), np.float32)
+    pads[:, 5:] = 1.0  # encoders_test.py:304-305
+    v, t, out = orc.video_clip(var["params"], cfg, x, ids, pads, "f64", return_intermediate=True)
+    arrays = {f"param/{k}": a for k, a in flat.items()}
+    arrays.update(inputs=x, text_token_ids=ids, text_paddings=pads, video_embeddings=v, text_embeddings=t,
+                  frame_embeddings=out["frame_embeddings"],
+                  spatiotemporal_features=out["spatiotemporal_features"])
+    np.savez_compressed(os.path.join(HERE, "g5_clip_tiny.npz"), **arrays)
+
+
 if __name__ == "__main__":
     g1_tiny()
     g2_base_dims()
     g4_ops()
+    g5_clip_tiny()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -22,7 +22,7 @@ def header_symbols():
 def test_library_present_and_loads():
     assert os.path.exists(_native.library_path()), "build with __graft_entry__.build()"
     lib = _native.load()
-    assert lib.vp_abi_version() == 2
+    assert lib.vp_abi_version() == 3
 
 
 def test_every_header_symbol_exported():

@@ -31,8 +31,10 @@ def test_get_model_and_errors():
     with pytest.raises(ValueError, match="not found"):
         models.get_model("videoprism_public_v1_giant")
     lvt = models.get_model("videoprism_lvt_public_v1_base")
-    with pytest.raises(NotImplementedError):
-        lvt.apply({}, None)
+    assert isinstance(lvt, encoders.FactorizedVideoCLIP)
+    assert (lvt.model_dim, lvt.num_auxiliary_layers, lvt.vocabulary_size) == (768, 2, 32000)
+    with pytest.raises(ValueError, match="missing parameters"):
+        lvt.engine({"params": {}}, 0)
 
 
 def test_init_leaf_count_and_shapes():

@@ -121,3 +121,100 @@ def factorized_encoder(params, video, cfg, frame_paddings=None):
     feats = _ln(feats, params["temporal_ln"])
     out = feats.reshape(b, m * n, t, D).permute(0, 2, 1, 3).reshape(b, t * m * n, D)
     return out.numpy(), spatial.numpy()
+
+
+# ----------------------------------------------------------------------------------------
+# LvT video-text model (encoders.py:656-910, layers.py:92-179, :502-527, :1044-1136)
+# ----------------------------------------------------------------------------------------
+def _stack_general(x, st, L, heads, cap, paddings, causal, act):
+    """Pre-LN stack with the merged causal/padding mask: key s is visible to query t iff
+    neither is padded and s <= t; a query with no visible key attends uniformly."""
+    xl = st["x_layers"]
+    B, S, D = x.shape
+    dh = D // heads
+    pad = torch.zeros(B, S, dtype=torch.float64) if paddings is None else _t(paddings)
+    keyok = pad[:, None, :] < 0.5                                   # [B, 1, S]
+    if causal:
+        qok = pad[:, :, None] < 0.5                                 # [B, S, 1]
+        tri = torch.tril(torch.ones(S, S, dtype=torch.bool))[None]  # s <= t
+        visible = keyok & qok & tri                                 # [B, T, S]
+    else:
+        visible = keyok.expand(B, S, S)
+    visible = visible[:, None]                                      # [B, 1, T, S]
+    none = ~visible.any(dim=-1, keepdim=True)
+    for i in range(L):
+        sa = xl["self_attention"]
+        h = F.layer_norm(x, (D,), weight=_t(xl["layer_norm"]["scale"][i]) + 1.0,
+                         bias=_t(xl["layer_norm"]["bias"][i]), eps=1e-6)
+        q = torch.einsum("bsd,dnh->bsnh", h, _t(sa["query"]["w"][i])) + _t(sa["query"]["b"][i])
+        k = torch.einsum("bsd,dnh->bsnh", h, _t(sa["key"]["w"][i])) + _t(sa["key"]["b"][i])
+        v = torch.einsum("bsd,dnh->bsnh", h, _t(sa["value"]["w"][i])) + _t(sa["value"]["b"][i])
+        logits = torch.einsum("btnh,bsnh->bnts", q / dh ** 0.5, k)
+        if cap > 0:
+            logits = cap * torch.tanh(logits / cap)
+        logits = torch.where(visible | none, logits, torch.full_like(logits, -torch.inf))
+        logits = torch.where(none.expand_as(logits), torch.zeros_like(logits), logits)
+        enc = torch.einsum("bnts,bsnh->btnh", torch.softmax(logits, dim=-1), v)
+        x = x + torch.einsum("btnh,dnh->btd", enc, _t(sa["post"]["w"][i])) + _t(sa["post"]["b"][i])
+        ff = xl["ff_layer"]
+        y = F.layer_norm(x, (D,), weight=_t(ff["layer_norm"]["scale"][i]) + 1.0,
+                         bias=_t(ff["layer_norm"]["bias"][i]), eps=1e-6)
+        a = act(y @ _t(ff["ffn_layer1"]["linear"]["kernel"][i]) + _t(ff["ffn_layer1"]["linear"]["bias"][i]))
+        a = a * (1.0 - pad[..., None])
+        o = a @ _t(ff["ffn_layer2"]["linear"]["kernel"][i]) + _t(ff["ffn_layer2"]["linear"]["bias"][i])
+        x = x + o * (1.0 - pad[..., None])
+    return x
+
+
+def _gelu(a):
+    return 0.5 * a * (1.0 + torch.erf(a / 2 ** 0.5))
+
+
+def pooler(tokens, p, heads):
+    """AttenTokenPoolingLayer: one learned query, dh = 4D/heads, per-dim scale, no cap, LN."""
+    x = _t(tokens)
+    D = x.shape[-1]
+    pa = p["pooling_attention"]
+    dh = 4 * D // heads
+    q = torch.einsum("d,dnh->nh", _t(p["pooling_attention_query"])[0], _t(pa["query"]["w"]))
+    q = (q + _t(pa["query"]["b"])) * (1.442695041 / dh ** 0.5) * F.softplus(_t(pa["per_dim_scale"]["per_dim_scale"]))
+    k = torch.einsum("bsd,dnh->bsnh", x, _t(pa["key"]["w"])) + _t(pa["key"]["b"])
+    v = torch.einsum("bsd,dnh->bsnh", x, _t(pa["value"]["w"])) + _t(pa["value"]["b"])
+    probs = torch.softmax(torch.einsum("nh,bsnh->bns", q, k), dim=-1)
+    enc = torch.einsum("bns,bsnh->bnh", probs, v)
+    out = torch.einsum("bnh,dnh->bd", enc, _t(pa["post"]["w"])) + _t(pa["post"]["b"])
+    return _ln(out, p["pooling_attention_layer_norm"])
+
+
+def _l2n(x):
+    return x / torch.sqrt((x * x).sum(-1, keepdim=True) + 1e-12)
+
+
+def video_clip(params, cfg, video, ids, paddings, frame_paddings=None):
+    """-> (video_emb, text_emb, frame_emb), all L2-normalised, fp64 numpy."""
+    D, heads, cap = cfg["model_dim"], cfg["num_heads"], cfg["atten_logit_cap"]
+    vcfg = dict(cfg)
+    feats, _ = factorized_encoder(params["vision_encoder"], video, vcfg, frame_paddings)
+    x = _t(feats)
+    if cfg["num_auxiliary_layers"]:
+        x = _stack_general(x, params["auxiliary_encoder"]["transformers_stack"], cfg["num_auxiliary_layers"],
+                           heads, cap, None, False, _gelu)
+    pp = params["contrastive_vision_pooler"]
+    vemb = _l2n(pooler(x, pp, heads))
+    b, t = video.shape[:2]
+    femb = _l2n(pooler(x.reshape(b * t, -1, D), pp, heads)).reshape(b, t, D)
+    te = params["text_encoder"]
+    idt = torch.as_tensor(ids, dtype=torch.long)
+    Q, L = idt.shape
+    emb = _t(te["token_emb"]["emb_var"])[idt.clamp(0, cfg["vocabulary_size"] - 1)] * D ** 0.5
+    pos = torch.arange(L, dtype=torch.float64)[:, None]
+    inv = torch.exp(torch.arange(D // 2, dtype=torch.float64) * -(torch.log(torch.tensor(1e4, dtype=torch.float64))
+                                                                  / max(D // 2 - 1, 1)))
+    emb = emb + torch.cat([torch.sin(pos * inv), torch.cos(pos * inv)], dim=-1)[None]
+    cls = _t(te["cls_emb"]).expand(Q, 1, D) * D ** 0.5
+    y = torch.cat([emb, cls], dim=1)
+    pad = torch.cat([_t(paddings), torch.zeros(Q, 1, dtype=torch.float64)], dim=1)
+    y = _stack_general(y, te["unimodal_transformer"], cfg["num_unimodal_layers"], heads, cap, pad,
+                       cfg["enable_causal_atten"], torch.relu)
+    temb = _l2n(_ln(y, te["unimodal_ln"])[:, -1])
+    return vemb.numpy(), temb.numpy(), femb.numpy()

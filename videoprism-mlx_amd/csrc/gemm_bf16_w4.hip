@@ -458,6 +458,7 @@ hipError_t w4_dispatch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, i
       if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, D, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_RESID_FFN_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RELU_BF16: return launch_w4<EPI_RELU_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

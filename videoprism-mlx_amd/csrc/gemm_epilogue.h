@@ -5,6 +5,7 @@
 // residual / position reads are the same width.  Semantics (layers.py line refs):
 //   EPI_BF16            out_bf16 = acc + bias                                   (:273-313)
 //   EPI_GELU_BF16       out_bf16 = gelu(acc + bias) * keep                      (:370-400)
+//   EPI_RELU_BF16       out_bf16 = relu(acc + bias) * keep   (text tower ffn_layer1, encoders.py:743)
 //   EPI_RESID_F32/_FFN  out_f32  = resid_f32 + (acc + bias) * keep              (:855, :425)
 //   EPI_POS_F32         out_f32  = acc + bias + pos[row % pos_rows]     (encoders.py:505-514)
 //   EPI_RESID_BF16/_FFN_BF16, EPI_POS_BF16: the same with a bf16 residual stream (fprop_dtype
@@ -26,7 +27,8 @@ struct EpiTraits {
                                      EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST;
   static constexpr bool kPos = EPI == EPI_POS_F32 || EPI == EPI_POS_BF16 || EPI == EPI_POS_BF16_ST;
   static constexpr bool kExtra = kResidF32 || kResidBf16 || kPos;
-  static constexpr bool kKeep = kGelu || kResidF32 || kResidBf16;
+  static constexpr bool kRelu = EPI == EPI_RELU_BF16;
+  static constexpr bool kKeep = kGelu || kRelu || kResidF32 || kResidBf16;
   static constexpr bool kOutBf16 = !(EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN || EPI == EPI_POS_F32);
 };
 
@@ -94,6 +96,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ep, int row, int n, flo
                                           float4 extra) {
   using Tr = EpiTraits<EPI>;
   if constexpr (Tr::kGelu) v = gelu4(v);
+  if constexpr (Tr::kRelu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
   if constexpr (Tr::kKeep) {
     v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep;
   }
@@ -135,8 +138,10 @@ __device__ __forceinline__ F8 epi_extra8(const EpiArgs& ep, int row, int n, int 
   return e;
 }
 
-__device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, bool gelu, bool kp, bool ex) {
+__device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, bool gelu, bool kp, bool ex,
+                                           bool relu = false) {
   if (gelu) v = gelu4(v);
+  if (relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
   if (kp) { v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep; }
   if (ex) { v.x += extra.x; v.y += extra.y; v.z += extra.z; v.w += extra.w; }
   return v;
@@ -151,8 +156,8 @@ typedef unsigned epi_u32x4 __attribute__((ext_vector_type(4)));
 template <int EPI, bool NT = true>
 __device__ __forceinline__ epi_u32x4 epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
   using Tr = EpiTraits<EPI>;
-  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra);
-  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra);
+  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra, Tr::kRelu);
+  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra, Tr::kRelu);
   epi_u32x4 pk = {0u, 0u, 0u, 0u};
   if constexpr (Tr::kOutBf16) {
     pk = epi_u32x4{pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),

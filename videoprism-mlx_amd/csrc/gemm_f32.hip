@@ -22,8 +22,12 @@ __device__ __forceinline__ void epi_f32(const EpiArgs& ep, int N, int m, int n, 
   float* out = static_cast<float*>(ep.out) + (int64_t)m * ep.ldo + n;
   if constexpr (EPI == EPI_BF16) {
     *reinterpret_cast<float4*>(out) = make_float4(v0, v1, v2, v3);
-  } else if constexpr (EPI == EPI_GELU_BF16) {
-    v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+  } else if constexpr (EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
+    if constexpr (EPI == EPI_GELU_BF16) {
+      v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+    } else {
+      v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+    }
     if (ep.rowpad) {
       const float keep = 1.0f - ep.rowpad[m];
       v0 *= keep; v1 *= keep; v2 *= keep; v3 *= keep;
@@ -148,6 +152,7 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
     case EPI_RESID_F32: return launch<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_F32: return launch<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN: return launch<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RELU_BF16: return launch<EPI_RELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

@@ -1,0 +1,411 @@
+// C-ABI of the LvT video-text model, FactorizedVideoCLIP (encoders.py:762-910), on top of the
+// FactorizedEncoder handle (vp_abi.cpp) and the shared layer schedule (vp_internal.h).
+//
+//   video: vision encoder (vp_forward) -> auxiliary encoder (2 pre-LN layers over all T*N
+//          tokens, attention_long_bf16) -> contrastive pooler (query folded into the key
+//          projection, clip_kernels.hip) -> LayerNorm -> L2 normalise
+//   text:  token embedding * sqrt(D) + sinusoidal positions, CLS appended -> 12 causal pre-LN
+//          ReLU layers (attention_masked) -> unimodal_ln on the CLS row -> L2 normalise
+#include "vp_internal.h"
+
+using namespace vpi;
+
+namespace {
+constexpr int kMaxTextLen = 1024;  // L + 1 (CLS) tokens; TEXT_MAX_LEN is 64 (models.py:53)
+}
+
+struct vp_clip {
+  vp_clip_config cfg;
+  int device = 0;
+  bool finalized = false;
+  vp_handle* video = nullptr;  // 'vision_encoder/' leaves
+  std::map<std::string, vpi::HostParam> host;
+  std::vector<std::string> names;
+  std::map<std::string, std::vector<int64_t>> expected;
+  std::vector<vpi::DevBuf> allocs;
+  bool bf16() const { return cfg.video.fprop_dtype == VP_BF16; }
+  std::vector<vpi::LayerW> aux, text;
+  // contrastive pooler (fp32): U [H][D], Wv^T [H][D][dp], bv [H][dp], Wpost^T [H*dp][D], bpost [D]
+  float *pU = nullptr, *pWvT = nullptr, *pbv = nullptr, *pWpT = nullptr, *pbp = nullptr;
+  float *pln_g = nullptr, *pln_b = nullptr;
+  // text tower: token table [V][D] (fprop dtype), cls [D], sinusoidal table [kMaxTextLen][D]
+  void* tok = nullptr;
+  float *cls = nullptr, *tpos = nullptr, *uln_g = nullptr, *uln_b = nullptr;
+};
+
+namespace {
+
+struct ClipVideoWs {
+  size_t inner = 0, feat = 0, logits = 0, stats = 0, zpart = 0, z = 0, enc = 0, pooled = 0, total = 0;
+};
+
+ClipVideoWs clip_video_ws(const vp_clip* c, int64_t B, int64_t T, int64_t H, int64_t W, size_t inner_bytes) {
+  const vp_config& v = c->cfg.video;
+  const int64_t P = v.patch_size, N = (H / P) * (W / P), M = B * T * N;
+  const int64_t D = v.model_dim, NH = v.num_heads, dp = 4 * D / NH;
+  const size_t es = c->bf16() ? 2 : 4;
+  const int64_t gc = std::max<int64_t>(B * vp::pool_chunks((int)(T * N)), B * T * vp::pool_chunks((int)N));
+  ClipVideoWs L;
+  size_t off = 0;
+  L.inner = off; off = align256(off + inner_bytes);
+  L.feat = off; off = align256(off + (size_t)M * D * es);
+  L.logits = off; off = align256(off + (size_t)M * NH * 4);
+  L.stats = off; off = align256(off + (size_t)B * T * NH * 8);
+  L.zpart = off; off = align256(off + (size_t)gc * NH * D * 4);
+  L.z = off; off = align256(off + (size_t)B * T * NH * D * 4);
+  L.enc = off; off = align256(off + (size_t)B * T * NH * dp * 4);
+  L.pooled = off; off = align256(off + (size_t)B * T * D * 4);
+  L.total = off;
+  return L;
+}
+
+struct ClipTextWs {
+  size_t x = 0, hb = 0, big = 0, pad = 0, total = 0;
+  int64_t Mt = 0;
+};
+
+ClipTextWs clip_text_ws(const vp_clip* c, int64_t Q, int64_t L) {
+  const int64_t D = c->cfg.video.model_dim;
+  const size_t es = c->bf16() ? 2 : 4;
+  ClipTextWs w;
+  w.Mt = (Q * (L + 1) + 255) / 256 * 256;
+  size_t off = 0;
+  w.x = off; off = align256(off + (size_t)w.Mt * D * 4);  // fp32 residual stream
+  w.hb = off; off = align256(off + (size_t)w.Mt * D * es);
+  w.big = off; off = align256(off + (size_t)w.Mt * 4 * D * es);
+  w.pad = off; off = align256(off + (size_t)w.Mt * 4);
+  w.total = off;
+  return w;
+}
+
+void build_clip_expected(vp_clip* c) {
+  const vp_clip_config& cc = c->cfg;
+  const int64_t D = cc.video.model_dim, NH = cc.video.num_heads, dp = 4 * D / NH;
+  if (cc.num_auxiliary_layers > 0)
+    add_stack_expected(c, "auxiliary_encoder/transformers_stack/x_layers/", cc.num_auxiliary_layers, D,
+                       cc.video.mlp_dim, NH);
+  const std::string pre = "contrastive_vision_pooler/";
+  add_expected(c, pre + "pooling_attention_query", {1, D});
+  add_expected(c, pre + "pooling_attention/per_dim_scale/per_dim_scale", {dp});
+  for (const char* q : {"query", "key", "value"}) {
+    add_expected(c, pre + "pooling_attention/" + q + "/w", {D, NH, dp});
+    add_expected(c, pre + "pooling_attention/" + q + "/b", {NH, dp});
+  }
+  add_expected(c, pre + "pooling_attention/post/w", {D, NH, dp});
+  add_expected(c, pre + "pooling_attention/post/b", {D});
+  add_expected(c, pre + "pooling_attention_layer_norm/scale", {D});
+  add_expected(c, pre + "pooling_attention_layer_norm/bias", {D});
+  add_expected(c, "text_encoder/token_emb/emb_var", {(int64_t)cc.vocabulary_size, D});
+  add_expected(c, "text_encoder/cls_emb", {1, 1, D});
+  add_stack_expected(c, "text_encoder/unimodal_transformer/x_layers/", cc.num_unimodal_layers, D, 4 * D, NH);
+  add_expected(c, "text_encoder/unimodal_ln/scale", {D});
+  add_expected(c, "text_encoder/unimodal_ln/bias", {D});
+}
+
+// AttenTokenPoolingLayer (layers.py:1044-1136) with the query folded into the key projection
+// (see clip_kernels.hip): host packing in fp64.
+int pack_pooler(vp_clip* c) {
+  const int64_t D = c->cfg.video.model_dim, H = c->cfg.video.num_heads, dp = 4 * D / H;
+  const std::string pre = "contrastive_vision_pooler/pooling_attention/";
+  const auto& query = param_data(c, "contrastive_vision_pooler/pooling_attention_query");
+  const auto& wq = param_data(c, pre + "query/w");
+  const auto& bq = param_data(c, pre + "query/b");
+  const auto& wk = param_data(c, pre + "key/w");
+  const auto& wv = param_data(c, pre + "value/w");
+  const auto& bv = param_data(c, pre + "value/b");
+  const auto& wp = param_data(c, pre + "post/w");
+  const auto& bp = param_data(c, pre + "post/b");
+  const auto& pds = param_data(c, pre + "per_dim_scale/per_dim_scale");
+  // q~[h][j] = (query . Wq[:, h, j] + bq[h][j]) * 1.442695041/sqrt(dp) * softplus(pds[j])  (:502-527)
+  std::vector<double> qt((size_t)H * dp);
+  const double r_softplus_0 = 1.442695041 / std::sqrt((double)dp);
+  for (int64_t h = 0; h < H; ++h)
+    for (int64_t j = 0; j < dp; ++j) {
+      double a = bq[(size_t)h * dp + j];
+      for (int64_t d = 0; d < D; ++d) a += (double)query[d] * wq[((size_t)d * H + h) * dp + j];
+      const double x = pds[j];
+      const double sp = x > 30.0 ? x : std::log1p(std::exp(x));
+      qt[(size_t)h * dp + j] = a * r_softplus_0 * sp;
+    }
+  std::vector<float> U((size_t)H * D), wvt((size_t)H * D * dp), wpt((size_t)H * dp * D);
+  for (int64_t h = 0; h < H; ++h)
+    for (int64_t d = 0; d < D; ++d) {
+      double a = 0.0;
+      for (int64_t j = 0; j < dp; ++j) a += (double)wk[((size_t)d * H + h) * dp + j] * qt[(size_t)h * dp + j];
+      U[(size_t)h * D + d] = (float)a;
+      for (int64_t j = 0; j < dp; ++j) wvt[((size_t)h * D + d) * dp + j] = wv[((size_t)d * H + h) * dp + j];
+    }
+  for (int64_t n = 0; n < D; ++n)
+    for (int64_t k = 0; k < H * dp; ++k) wpt[(size_t)k * D + n] = wp[(size_t)n * H * dp + k];
+  std::vector<float> g(D);
+  const auto& sc = param_data(c, "contrastive_vision_pooler/pooling_attention_layer_norm/scale");
+  for (int64_t d = 0; d < D; ++d) g[d] = sc[d] + 1.0f;
+  int rc;
+  if ((rc = upload_f32(c, U, &c->pU)) || (rc = upload_f32(c, wvt, &c->pWvT)) || (rc = upload_f32(c, bv, &c->pbv)) ||
+      (rc = upload_f32(c, wpt, &c->pWpT)) || (rc = upload_f32(c, bp, &c->pbp)) || (rc = upload_f32(c, g, &c->pln_g)) ||
+      (rc = upload_f32(c, param_data(c, "contrastive_vision_pooler/pooling_attention_layer_norm/bias"), &c->pln_b)))
+    return rc;
+  return VP_OK;
+}
+
+int pack_text(vp_clip* c) {
+  const int64_t D = c->cfg.video.model_dim;
+  int rc;
+  if ((rc = upload_mat(c, param_data(c, "text_encoder/token_emb/emb_var"), &c->tok))) return rc;
+  if ((rc = upload_f32(c, param_data(c, "text_encoder/cls_emb"), &c->cls))) return rc;
+  // PositionalEmbedding (encoders.py:190-224): [sin(t * inv) | cos(t * inv)], zero column for odd D
+  std::vector<float> pos((size_t)kMaxTextLen * D, 0.0f);
+  const int64_t nts = D / 2;
+  const double inc = std::log(10000.0) / std::max<double>((double)nts - 1.0, 1.0);
+  for (int t = 0; t < kMaxTextLen; ++t)
+    for (int64_t i = 0; i < nts; ++i) {
+      const double st = t * std::exp(-(double)i * inc);
+      pos[(size_t)t * D + i] = (float)std::sin(st);
+      pos[(size_t)t * D + nts + i] = (float)std::cos(st);
+    }
+  if ((rc = upload_f32(c, pos, &c->tpos))) return rc;
+  std::vector<float> g(D);
+  const auto& sc = param_data(c, "text_encoder/unimodal_ln/scale");
+  for (int64_t d = 0; d < D; ++d) g[d] = sc[d] + 1.0f;
+  if ((rc = upload_f32(c, g, &c->uln_g)) || (rc = upload_f32(c, param_data(c, "text_encoder/unimodal_ln/bias"), &c->uln_b)))
+    return rc;
+  const int NH = c->cfg.video.num_heads;
+  return pack_stack(c, "text_encoder/unimodal_transformer/x_layers/", c->cfg.num_unimodal_layers, D, 4 * D, NH,
+                    false, c->text);
+}
+
+}  // namespace
+
+extern "C" {
+
+int vp_clip_create(const vp_clip_config* cfg, int device, vp_clip** out) {
+  if (!cfg || !out) return fail(VP_EINVAL, "null argument");
+  *out = nullptr;
+  if (cfg->num_auxiliary_layers < 0 || cfg->num_unimodal_layers < 0 || cfg->vocabulary_size < 1)
+    return fail(VP_EINVAL, "bad LvT configuration");
+  if (cfg->video.num_heads > 16) return fail(VP_ENOTSUP, "pooler kernels support up to 16 heads");
+  vp_handle* v = nullptr;
+  int rc = vp_create(&cfg->video, device, &v);
+  if (rc) return rc;
+  v->prefix = "vision_encoder/";
+  v->names.clear();
+  v->expected.clear();
+  build_expected(v);
+  vp_clip* c = new vp_clip();
+  c->cfg = *cfg;
+  c->device = device;
+  c->video = v;
+  build_clip_expected(c);
+  *out = c;
+  return VP_OK;
+}
+
+int vp_clip_destroy(vp_clip* c) {
+  if (!c) return VP_OK;
+  vp_destroy(c->video);
+  hipSetDevice(c->device);
+  for (auto& a : c->allocs) hipFree(a.p);
+  delete c;
+  return VP_OK;
+}
+
+int vp_clip_set_param(vp_clip* c, const char* name, const float* host_data, const int64_t* shape, int ndim) {
+  if (!c || !name || !host_data || (ndim > 0 && !shape)) return fail(VP_EINVAL, "null argument");
+  if (c->finalized) return fail(VP_ESTATE, "handle already finalized");
+  if (!std::strncmp(name, "vision_encoder/", 15)) return vp_set_param(c->video, name, host_data, shape, ndim);
+  auto it = c->expected.find(name);
+  if (it == c->expected.end()) return fail(VP_EINVAL, std::string("unexpected parameter: ") + name);
+  const auto& exp = it->second;
+  bool ok = (int)exp.size() == ndim;
+  for (int i = 0; ok && i < ndim; ++i) ok = exp[i] == shape[i];
+  if (!ok) {
+    std::string e = std::string("shape mismatch for ") + name + ": expected (";
+    for (size_t i = 0; i < exp.size(); ++i) e += std::to_string(exp[i]) + (i + 1 < exp.size() ? ", " : "");
+    e += ") got (";
+    for (int i = 0; i < ndim; ++i) e += std::to_string(shape[i]) + (i + 1 < ndim ? ", " : "");
+    return fail(VP_EINVAL, e + ")");
+  }
+  size_t n = 1;
+  for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
+  HostParam hp;
+  hp.shape.assign(shape, shape + ndim);
+  hp.data.assign(host_data, host_data + n);
+  c->host[name] = std::move(hp);
+  return VP_OK;
+}
+
+int vp_clip_param_count(const vp_clip* c, int* count) {
+  if (!c || !count) return fail(VP_EINVAL, "null argument");
+  *count = (int)(c->video->names.size() + c->names.size());
+  return VP_OK;
+}
+
+int vp_clip_param_name(const vp_clip* c, int index, const char** name) {
+  if (!c || !name || index < 0) return fail(VP_EINVAL, "bad index");
+  const int nv = (int)c->video->names.size();
+  if (index < nv) {
+    *name = c->video->names[index].c_str();
+    return VP_OK;
+  }
+  if (index - nv >= (int)c->names.size()) return fail(VP_EINVAL, "bad index");
+  *name = c->names[index - nv].c_str();
+  return VP_OK;
+}
+
+int vp_clip_finalize(vp_clip* c) {
+  if (!c) return fail(VP_EINVAL, "null handle");
+  if (c->finalized) return VP_OK;
+  for (const auto& n : c->names)
+    if (!c->host.count(n)) return fail(VP_ESTATE, "missing parameter: " + n);
+  int rc = vp_finalize(c->video);
+  if (rc) return rc;
+  VP_HIP(hipSetDevice(c->device));
+  const vp_config& v = c->cfg.video;
+  if (c->cfg.num_auxiliary_layers > 0 &&
+      (rc = pack_stack(c, "auxiliary_encoder/transformers_stack/x_layers/", c->cfg.num_auxiliary_layers, v.model_dim,
+                       v.mlp_dim, v.num_heads, c->bf16(), c->aux)))
+    return rc;
+  if ((rc = pack_pooler(c)) || (rc = pack_text(c))) return rc;
+  c->host.clear();
+  c->finalized = true;
+  return VP_OK;
+}
+
+int vp_clip_video_handle(vp_clip* c, vp_handle** video) {
+  if (!c || !video) return fail(VP_EINVAL, "null argument");
+  *video = c->video;
+  return VP_OK;
+}
+
+int vp_clip_video_workspace_bytes(const vp_clip* c, int64_t B, int64_t T, int64_t H, int64_t W, size_t* bytes) {
+  if (!c || !bytes) return fail(VP_EINVAL, "null argument");
+  size_t inner = 0;
+  int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
+  if (rc) return rc;
+  *bytes = clip_video_ws(c, B, T, H, W, inner).total;
+  return VP_OK;
+}
+
+int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H, int64_t W,
+                         const float* frame_paddings, int normalize, float* video_emb, float* frame_emb,
+                         void* spatial_out, void* spatiotemporal_out, int out_dtype, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  using namespace vp;
+  if (!c || !video || !video_emb || !workspace) return fail(VP_EINVAL, "null argument");
+  if (!c->finalized) return fail(VP_ESTATE, "vp_clip_finalize has not been called");
+  const bool bf = c->bf16();
+  const int fdt = bf ? VP_BF16 : VP_F32;
+  if (spatiotemporal_out && out_dtype != fdt)
+    return fail(VP_EINVAL, "spatiotemporal_features are returned in the fprop dtype");
+  size_t inner = 0;
+  int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
+  if (rc) return rc;
+  const ClipVideoWs L = clip_video_ws(c, B, T, H, W, inner);
+  if (ws_bytes < L.total) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(L.total));
+  const vp_config& v = c->cfg.video;
+  const int P = v.patch_size, N = (int)((H / P) * (W / P)), D = v.model_dim, NH = v.num_heads, dp = 4 * D / NH;
+  const int S = (int)T * N;
+  const int64_t M64 = B * T * N;
+  if (M64 > 0x7fffffff) return fail(VP_ENOTSUP, "too many tokens");
+  const int M = (int)M64;
+  if (!bf && c->cfg.num_auxiliary_layers > 0 && M % 128) return fail(VP_ENOTSUP, "fp32 GEMM needs B*T*N % 128 == 0");
+  char* ws = static_cast<char*>(workspace);
+  void* feat = ws + L.feat;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // 1. vision encoder -> vision_features [B, T*N, D] (encoders.py:833-845)
+  rc = vp_forward(c->video, video, in_dtype, B, T, H, W, frame_paddings, feat, fdt, spatial_out, ws + L.inner,
+                  inner, stream);
+  if (rc) return rc;
+  VP_HIP(hipSetDevice(c->device));
+  const size_t es = bf ? 2 : 4;
+  if (spatiotemporal_out)
+    VP_HIP(hipMemcpyAsync(spatiotemporal_out, feat, (size_t)M * D * es, hipMemcpyDeviceToDevice, s));
+  // the vision encoder's scratch regions are free again (stream order): reuse them
+  const WsLayout Lv = ws_layout(c->video, B, T, H, W);
+  char* wsv = ws + L.inner;
+  Fwd f;
+  f.s = s; f.bf = bf; f.M = M; f.D = D; f.NH = NH; f.cap = v.atten_logit_cap;
+  f.hb = wsv + Lv.hbuf; f.big = wsv + Lv.big;
+  f.st_part = reinterpret_cast<float*>(wsv + Lv.st_part);
+  f.ln_rs = reinterpret_cast<float*>(wsv + Lv.ln_rs);
+  f.pf = &c->video->prof;
+  // 2. auxiliary encoder over all T*N tokens of each clip (encoders.py:846-857; paddings None)
+  if (c->cfg.num_auxiliary_layers > 0) {
+    if (bf) {
+      if (S % 256) return fail(VP_ENOTSUP, "bf16 auxiliary attention needs T*N % 256 == 0");
+      VP_HIP(f.rec(PC_LAYERNORM, 0.0, (double)M * D * 2, [&] {
+        return ln_row_stats((const bf16_t*)feat, M, D, f.ln_rs, s); }));
+    }
+    rc = f.run_stack(c->aux, feat, (int)B, S, nullptr, v.mlp_dim, PC_ATTN_AUX, ATT_LONG, bf, false);
+    if (rc) return rc;
+  }
+  // 3. contrastive pooler + L2 (encoders.py:859-872), and per frame (:874-885)
+  float* logits = reinterpret_cast<float*>(ws + L.logits);
+  float* stats = reinterpret_cast<float*>(ws + L.stats);
+  float* zpart = reinterpret_cast<float*>(ws + L.zpart);
+  float* z = reinterpret_cast<float*>(ws + L.z);
+  float* enc = reinterpret_cast<float*>(ws + L.enc);
+  float* pooled = reinterpret_cast<float*>(ws + L.pooled);
+  auto pool = [&](int G, int Sg, float* dst) -> int {
+    const double bytes = 2.0 * M * D * es;  // two streaming passes over the tokens
+    VP_HIP(f.rec(PC_POOL, 2.0 * 2.0 * M * D * NH, bytes, [&] {
+      hipError_t e = pool_logits(feat, bf, M, Sg, D, c->pU, NH, logits, s);
+      if (e != hipSuccess) return e;
+      return pool_softmax_wsum(feat, bf, G, Sg, D, NH, logits, stats, zpart, z, s); }));
+    VP_HIP(small_gemm(z, (int64_t)NH * D, D, c->pWvT, (int64_t)D * dp, c->pbv, dp, enc, (int64_t)NH * dp, dp, G, dp,
+                      D, NH, s));
+    VP_HIP(small_gemm(enc, (int64_t)NH * dp, 0, c->pWpT, 0, c->pbp, 0, pooled, D, 0, G, D, NH * dp, 1, s));
+    VP_HIP(ln_l2_rows(pooled, 0, D, G, D, c->pln_g, c->pln_b, normalize, dst, s));
+    return VP_OK;
+  };
+  if ((rc = pool((int)B, S, video_emb))) return rc;
+  if (frame_emb && (rc = pool((int)(B * T), N, frame_emb))) return rc;
+  return VP_OK;
+}
+
+int vp_clip_text_workspace_bytes(const vp_clip* c, int64_t Q, int64_t L, size_t* bytes) {
+  if (!c || !bytes) return fail(VP_EINVAL, "null argument");
+  if (Q < 1 || L < 1 || L + 1 > kMaxTextLen) return fail(VP_EINVAL, "text ids must be [Q, L] with 1 <= L < 1024");
+  *bytes = clip_text_ws(c, Q, L).total;
+  return VP_OK;
+}
+
+int vp_clip_encode_text(vp_clip* c, const int32_t* ids, const float* paddings, int64_t Q, int64_t L, int normalize,
+                        float* text_emb, void* workspace, size_t ws_bytes, void* stream) {
+  using namespace vp;
+  if (!c || !ids || !paddings || !text_emb || !workspace) return fail(VP_EINVAL, "null argument");
+  if (!c->finalized) return fail(VP_ESTATE, "vp_clip_finalize has not been called");
+  if (Q < 1 || L < 1 || L + 1 > kMaxTextLen) return fail(VP_EINVAL, "text ids must be [Q, L] with 1 <= L < 1024");
+  const ClipTextWs w = clip_text_ws(c, Q, L);
+  if (ws_bytes < w.total) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(w.total));
+  if (w.Mt > 0x7fffffff) return fail(VP_ENOTSUP, "too many text tokens");
+  VP_HIP(hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool bf = c->bf16();
+  const vp_config& v = c->cfg.video;
+  const int D = v.model_dim;
+  char* ws = static_cast<char*>(workspace);
+  void* x = ws + w.x;
+  float* pad = reinterpret_cast<float*>(ws + w.pad);
+  // The text tower keeps its residual stream in fp32 in both modes (bf16 GEMM operands, fp32
+  // sums): its Q*(L+1) rows cost nothing, and it removes the stream's per-layer bf16 rounding.
+  // Rows past Q*(L+1) only pad the GEMMs' M to a tile multiple: keep them finite.
+  VP_HIP(hipMemsetAsync(x, 0, (size_t)w.Mt * D * 4, s));
+  VP_HIP(hipMemsetAsync(pad, 0, (size_t)w.Mt * 4, s));
+  VP_HIP(text_embed(ids, (int)Q, (int)L, c->tok, bf, c->cfg.vocabulary_size, c->cls, c->tpos, std::sqrt((float)D), D,
+                    x, 0, paddings, pad, s));
+  Fwd f;
+  f.s = s; f.bf = bf; f.M = (int)w.Mt; f.D = D; f.NH = v.num_heads; f.cap = v.atten_logit_cap;
+  f.causal = c->cfg.enable_causal_atten ? 1 : 0;
+  f.xs_f32 = true;
+  f.hb = ws + w.hb; f.big = ws + w.big;
+  f.pf = &c->video->prof;
+  int rc = f.run_stack(c->text, x, (int)Q, (int)L + 1, pad, 4 * D, PC_ATTN_TEXT, ATT_TEXT, false, true);
+  if (rc) return rc;
+  // unimodal_ln on the CLS rows, then L2 (encoders.py:752-758, :905-908)
+  VP_HIP(ln_l2_rows(static_cast<float*>(x) + (size_t)L * D, 0, (int64_t)(L + 1) * D, (int)Q, D, c->uln_g,
+                    c->uln_b, normalize, text_emb, s));
+  return VP_OK;
+}
+
+}  // extern "C"

@@ -29,6 +29,9 @@ enum Epilogue {
   EPI_RESID_BF16_ST = 10,
   EPI_RESID_FFN_BF16_ST = 11,
   EPI_POS_BF16_ST = 12,
+  // ReLU FFN of the text tower (encoders.py:743): out = relu(acc + bias) * (1 - rowpad);
+  // bf16 out on the bf16 GEMM, fp32 out on the fp32 GEMM
+  EPI_RELU_BF16 = 13,
 };
 
 struct EpiArgs {
@@ -109,6 +112,37 @@ hipError_t expand_paddings(const float* frame_pad, int B, int T, int Nsp, float*
 hipError_t ln_stats_finalize(const float* st_part, int P, int64_t M, float* ln_rs, hipStream_t s);
 // same statistics straight from bf16 rows [M][D] (two-pass), for tests and the op API
 hipError_t ln_row_stats(const bf16_t* x, int64_t M, int D, float* ln_rs, hipStream_t s);
+
+// ---- LvT video-text path (attention_long.hip, clip_kernels.hip) ----
+// auxiliary-encoder self-attention over S = T*N tokens (S % 256 == 0), capped, no masks
+hipError_t attention_long_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap,
+                               hipStream_t s);
+// generic fp32-math attention (any S, dh 64) with key paddings and the causal merge of
+// layers.py:111-179; qkv / o in bf16 (in_is_bf16) or fp32
+hipError_t attention_masked(const void* qkv, void* o, int in_is_bf16, int num_seq, int S, int heads,
+                            float cap, const float* key_pad, int causal, hipStream_t s);
+// contrastive pooler: logits[g][h][s] = x[g*S+s] . U[h]; then softmax per (g,h) and
+// z[g][h][:] = sum_s p x (zpart scratch: [G][pool_chunks(S)][H][D], stats [G*H][2])
+hipError_t pool_logits(const void* x, int in_bf16, int64_t rows, int S, int D, const float* U, int H,
+                       float* logits, hipStream_t s);
+hipError_t pool_softmax_wsum(const void* x, int in_bf16, int G, int S, int D, int H, const float* logits,
+                             float* stats, float* zpart, float* z, hipStream_t s);
+int pool_chunks(int S);
+// out[b][m][n] = A[b][m][:] . Wt[b][:][n] + bias[b][n] (fp32, small M), batch strides sA/sW/sB/sO
+hipError_t small_gemm(const float* A, int64_t lda, int64_t sA, const float* Wt, int64_t sW, const float* bias,
+                      int64_t sB, float* out, int64_t ldo, int64_t sO, int M, int N, int K, int batch,
+                      hipStream_t s);
+// rows r of x (stride elements apart): optional LayerNorm (gamma = 1 + scale) then optional
+// L2 normalisation, fp32 out [rows][D]
+hipError_t ln_l2_rows(const void* x, int in_bf16, int64_t stride, int rows, int D, const float* gamma,
+                      const float* beta, int do_l2, float* out, hipStream_t s);
+// text tokens: out[q*(L+1)+t] = table[ids[q][t]]*scale + pos[t] (t < L), cls*scale (t = L);
+// pad_out[q*(L+1)+t] = pad_in[q][t] (t < L), 0 (t = L)
+hipError_t text_embed(const int32_t* ids, int Q, int L, const void* table, int table_bf16, int V, const float* cls,
+                      const float* pos, float scale, int D, void* out, int out_bf16, const float* pad_in,
+                      float* pad_out, hipStream_t s);
+// out[i][j] = a[i] . b[j]
+hipError_t similarity(const float* a, const float* b, int B, int Q, int D, float* out, hipStream_t s);
 
 hipError_t pool_l2(const void* emb, int is_bf16, int B, int L, int D, float* out, hipStream_t s);
 

@@ -49,6 +49,16 @@ class vp_config(ctypes.Structure):
     ]
 
 
+class vp_clip_config(ctypes.Structure):
+    _fields_ = [
+        ("video", vp_config),
+        ("num_auxiliary_layers", c_int32),
+        ("vocabulary_size", c_int32),
+        ("num_unimodal_layers", c_int32),
+        ("enable_causal_atten", c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     "vp_last_error": (c_char_p, []),
@@ -77,6 +87,25 @@ _SIGNATURES = {
     "vp_op_patchify": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64,
                                c_int64, c_int64, c_void_p]),
     "vp_op_pool_l2": (c_int, [c_void_p, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+    "vp_op_attention_masked": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float,
+                                       c_void_p, c_int, c_void_p]),
+    "vp_op_similarity": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p]),
+    # LvT video-text model (FactorizedVideoCLIP)
+    "vp_clip_create": (c_int, [POINTER(vp_clip_config), c_int, POINTER(c_void_p)]),
+    "vp_clip_destroy": (c_int, [c_void_p]),
+    "vp_clip_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "vp_clip_param_count": (c_int, [c_void_p, POINTER(c_int)]),
+    "vp_clip_param_name": (c_int, [c_void_p, c_int, POINTER(c_char_p)]),
+    "vp_clip_finalize": (c_int, [c_void_p]),
+    "vp_clip_video_handle": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "vp_clip_video_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64,
+                                              POINTER(c_size_t)]),
+    "vp_clip_encode_video": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64,
+                                     c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                     c_void_p, c_size_t, c_void_p]),
+    "vp_clip_text_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_size_t)]),
+    "vp_clip_encode_text": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p,
+                                    c_void_p, c_size_t, c_void_p]),
     # not in the public header: named-kernel GEMM for A/B tests and tools/gemm_bench.py
     "vp_dev_gemm_kernel": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
@@ -212,6 +241,28 @@ def op_attention(qkv, num_seq, S, heads, cap, key_pad=None, out=None, stream=Non
         out = torch.empty((num_seq * S, D), dtype=qkv.dtype, device=qkv.device)
     call("vp_op_attention", _prec(qkv), _ptr(qkv), _ptr(out), num_seq, S, heads, float(cap),
          _ptr(key_pad), _stream(stream))
+    return out
+
+
+def op_attention_masked(qkv, num_seq, S, heads, cap, key_pad=None, causal=False, out=None,
+                        stream=None):
+    """Generic fp32-math attention with key paddings and the causal merge (text tower)."""
+    import torch
+    D = heads * 64
+    if out is None:
+        out = torch.empty((num_seq * S, D), dtype=qkv.dtype, device=qkv.device)
+    call("vp_op_attention_masked", _prec(qkv), _ptr(qkv), _ptr(out), num_seq, S, heads, float(cap),
+         _ptr(key_pad), 1 if causal else 0, _stream(stream))
+    return out
+
+
+def op_similarity(video_emb, text_emb, stream=None):
+    """video_emb [B, D] . text_emb [Q, D]^T (fp32)."""
+    import torch
+    B, D = video_emb.shape
+    Q = text_emb.shape[0]
+    out = torch.empty((B, Q), dtype=torch.float32, device=video_emb.device)
+    call("vp_op_similarity", _ptr(video_emb), _ptr(text_emb), B, Q, D, _ptr(out), _stream(stream))
     return out
 
 

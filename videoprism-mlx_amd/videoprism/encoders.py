@@ -37,6 +37,28 @@ def _is_bf16_dtype(dt) -> bool:
     return "bfloat16" in str(name) or "bfloat16" in str(dt)
 
 
+def _profile_enable(handle, capacity: int) -> None:
+    _native.call("vp_profile_enable", handle, int(capacity))
+
+
+def _profile_read(handle) -> dict:
+    """{kernel class: {ms, flops, bytes, launches}} since the previous read (vp_profile_read)."""
+    lib = _native.load()
+    n = lib.vp_profile_class_count()
+    ms = (ctypes.c_double * n)()
+    fl = (ctypes.c_double * n)()
+    by = (ctypes.c_double * n)()
+    la = (ctypes.c_int64 * n)()
+    _native.call("vp_profile_read", handle, n, ms, fl, by, la)
+    out = {}
+    for i in range(n):
+        name = ctypes.c_char_p()
+        _native.call("vp_profile_class_name", i, ctypes.byref(name))
+        if la[i]:
+            out[name.value.decode()] = dict(ms=ms[i], flops=fl[i], bytes=by[i], launches=la[i])
+    return out
+
+
 class Engine:
     """One vp_handle (packed weights on one device) plus a reusable workspace."""
 
@@ -76,23 +98,10 @@ class Engine:
 
     # -- live per-kernel timing (HIP events on the launch stream, vp_profile_*) ---------
     def profile_enable(self, capacity: int) -> None:
-        _native.call("vp_profile_enable", self._h, int(capacity))
+        _profile_enable(self._h, capacity)
 
     def profile_read(self) -> dict:
-        lib = _native.load()
-        n = lib.vp_profile_class_count()
-        ms = (ctypes.c_double * n)()
-        fl = (ctypes.c_double * n)()
-        by = (ctypes.c_double * n)()
-        la = (ctypes.c_int64 * n)()
-        _native.call("vp_profile_read", self._h, n, ms, fl, by, la)
-        out = {}
-        for i in range(n):
-            name = ctypes.c_char_p()
-            _native.call("vp_profile_class_name", i, ctypes.byref(name))
-            if la[i]:
-                out[name.value.decode()] = dict(ms=ms[i], flops=fl[i], bytes=by[i], launches=la[i])
-        return out
+        return _profile_read(self._h)
 
     def workspace(self, B, T, H, W):
         torch = _torch()
@@ -236,5 +245,246 @@ class FactorizedEncoder:
             emb = emb.float().cpu().numpy()
             outputs = {k: v.float().cpu().numpy() for k, v in outputs.items()}
         return emb, outputs
+
+    __call__ = apply
+
+
+class ClipEngine:
+    """One vp_clip handle (packed LvT weights on one device) plus reusable workspaces."""
+
+    def __init__(self, cfg: dict, flat_params: dict, device: int, bf16: bool):
+        self.cfg = dict(cfg)
+        self.device = device
+        self.bf16 = bf16
+        lib = _native.load()
+        v = _native.vp_config(
+            patch_size=cfg["patch_size"], pos_emb_t=cfg["pos_emb_shape"][0],
+            pos_emb_h=cfg["pos_emb_shape"][1], pos_emb_w=cfg["pos_emb_shape"][2],
+            model_dim=cfg["model_dim"], num_spatial_layers=cfg["num_spatial_layers"],
+            num_temporal_layers=cfg["num_temporal_layers"], num_heads=cfg["num_heads"],
+            mlp_dim=cfg["mlp_dim"], atten_logit_cap=float(cfg.get("atten_logit_cap", 0.0)),
+            fprop_dtype=_native.VP_BF16 if bf16 else _native.VP_F32)
+        c = _native.vp_clip_config(
+            video=v, num_auxiliary_layers=cfg.get("num_auxiliary_layers", 0),
+            vocabulary_size=cfg["vocabulary_size"],
+            num_unimodal_layers=cfg["num_unimodal_layers"],
+            enable_causal_atten=1 if cfg.get("enable_causal_atten", True) else 0)
+        h = ctypes.c_void_p()
+        _native.check(lib.vp_clip_create(ctypes.byref(c), device, ctypes.byref(h)))
+        self._h = h
+        try:
+            for name, arr in flat_params.items():
+                a = np.ascontiguousarray(arr, dtype=np.float32)
+                shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+                _native.check(lib.vp_clip_set_param(h, name.encode(),
+                                                    a.ctypes.data_as(ctypes.c_void_p), shape, a.ndim))
+            _native.check(lib.vp_clip_finalize(h))
+        except Exception:
+            lib.vp_clip_destroy(h)
+            self._h = None
+            raise
+        self._ws = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _native._lib is not None:
+            _native._lib.vp_clip_destroy(h)
+            self._h = None
+
+    def video_handle(self):
+        v = ctypes.c_void_p()
+        _native.call("vp_clip_video_handle", self._h, ctypes.byref(v))
+        return v
+
+    def profile_enable(self, capacity: int) -> None:
+        """HIP events around every launch of both towers (vision, auxiliary, pooler, text)."""
+        _profile_enable(self.video_handle(), capacity)
+
+    def profile_read(self) -> dict:
+        return _profile_read(self.video_handle())
+
+    def _workspace(self, key, nbytes):
+        torch = _torch()
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < nbytes:
+            self._ws[key] = None
+            ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=f"cuda:{self.device}")
+            self._ws[key] = ws
+        return ws
+
+    def encode_video(self, video, frame_paddings=None, normalize=True, want_frames=False,
+                     want_spatial=False, want_spatiotemporal=False, stream=None):
+        torch = _torch()
+        B, T, H, W, C = video.shape
+        if C != 3:
+            raise ValueError("inputs must have 3 channels")
+        P = self.cfg["patch_size"]
+        if H % P or W % P:
+            raise ValueError(f"Image height ({H}) and width ({W}) should be multiples "
+                             f"of patch_size ({P}).")
+        video = video.contiguous()
+        if video.dtype not in (torch.bfloat16, torch.float32):
+            video = video.float()
+        in_dt = _native.VP_BF16 if video.dtype == torch.bfloat16 else _native.VP_F32
+        D = self.cfg["model_dim"]
+        N = (H // P) * (W // P)
+        fdt = torch.bfloat16 if self.bf16 else torch.float32
+        dev = video.device
+        vemb = torch.empty((B, D), dtype=torch.float32, device=dev)
+        femb = torch.empty((B, T, D), dtype=torch.float32, device=dev) if want_frames else None
+        sp = torch.empty((B, T * N, D), dtype=fdt, device=dev) if want_spatial else None
+        st = torch.empty((B, T * N, D), dtype=fdt, device=dev) if want_spatiotemporal else None
+        fp = None
+        if frame_paddings is not None:
+            fp = frame_paddings.to(device=dev, dtype=torch.float32).contiguous()
+            if tuple(fp.shape) != (B, T):
+                raise AssertionError(f"frame_paddings.shape == {(B, T)} failed (encoders.py:442)")
+        n = ctypes.c_size_t()
+        _native.call("vp_clip_video_workspace_bytes", self._h, B, T, H, W, ctypes.byref(n))
+        ws = self._workspace("video", n.value)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _native.call("vp_clip_encode_video", self._h, ptr(video), in_dt, B, T, H, W, ptr(fp),
+                     1 if normalize else 0, ptr(vemb), ptr(femb), ptr(sp), ptr(st),
+                     _native.VP_BF16 if self.bf16 else _native.VP_F32, ptr(ws), ws.numel(),
+                     ctypes.c_void_p(s.cuda_stream))
+        return vemb, femb, sp, st
+
+    def encode_text(self, ids, paddings, normalize=True, stream=None):
+        torch = _torch()
+        Q, L = ids.shape
+        ids = ids.to(dtype=torch.int32).contiguous()
+        pad = paddings.to(device=ids.device, dtype=torch.float32).contiguous()
+        if tuple(pad.shape) != (Q, L):
+            raise ValueError(f"text_paddings must be [{Q}, {L}], got {tuple(pad.shape)}")
+        D = self.cfg["model_dim"]
+        out = torch.empty((Q, D), dtype=torch.float32, device=ids.device)
+        n = ctypes.c_size_t()
+        _native.call("vp_clip_text_workspace_bytes", self._h, Q, L, ctypes.byref(n))
+        ws = self._workspace("text", n.value)
+        s = stream if stream is not None else torch.cuda.current_stream(ids.device)
+        _native.call("vp_clip_encode_text", self._h, ctypes.c_void_p(ids.data_ptr()),
+                     ctypes.c_void_p(pad.data_ptr()), Q, L, 1 if normalize else 0,
+                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                     ctypes.c_void_p(s.cuda_stream))
+        return out
+
+
+@dataclasses.dataclass
+class FactorizedVideoCLIP:
+    """encoders.py:762-910 attributes (the LvT video-text model); `fprop_dtype` as set by
+    models.get_model."""
+
+    patch_size: int = 18
+    pos_emb_shape: tuple = (16, 16, 16)
+    num_spatial_layers: int = 12
+    num_temporal_layers: int = 4
+    mlp_dim: int = 3072
+    num_auxiliary_layers: int = 0
+    vocabulary_size: int = 128
+    enable_causal_atten: bool = True
+    num_unimodal_layers: int = 12
+    norm_policy: str = "pre"
+    model_dim: int = 768
+    num_heads: int = 12
+    atten_logit_cap: float = 0.0
+    scan: bool = False
+    fprop_dtype: Any = None
+    dtype: Any = None
+
+    def __post_init__(self):
+        self._engines: dict = {}
+
+    def config(self) -> dict:
+        return dict(patch_size=self.patch_size, pos_emb_shape=tuple(self.pos_emb_shape),
+                    num_spatial_layers=self.num_spatial_layers,
+                    num_temporal_layers=self.num_temporal_layers, mlp_dim=self.mlp_dim,
+                    num_auxiliary_layers=self.num_auxiliary_layers,
+                    vocabulary_size=self.vocabulary_size,
+                    enable_causal_atten=self.enable_causal_atten,
+                    num_unimodal_layers=self.num_unimodal_layers, model_dim=self.model_dim,
+                    num_heads=self.num_heads, atten_logit_cap=self.atten_logit_cap)
+
+    def param_specs(self) -> dict:
+        return params_lib.clip_leaf_specs(self.config(), scan=True)
+
+    @property
+    def is_bf16(self) -> bool:
+        return _is_bf16_dtype(self.fprop_dtype)
+
+    def init(self, rng=0, inputs=None, train: bool = False, **kwargs) -> dict:
+        del inputs, train, kwargs
+        seed = int(np.asarray(rng).ravel()[-1]) if not isinstance(rng, int) else rng
+        return params_lib.synthetic_params(self.config(), seed, specs=self.param_specs())
+
+    def engine(self, variables, device: int) -> ClipEngine:
+        p = variables["params"] if isinstance(variables, dict) and "params" in variables else variables
+        key = (id(p), device, self.is_bf16)
+        ent = self._engines.get(key)
+        if ent is not None and ent[0] is p:
+            return ent[1]
+        if self.norm_policy != "pre":
+            raise NotImplementedError("only norm_policy='pre' is implemented (public LvT configs)")
+        flat = params_lib.canonical_params(variables)
+        params_lib.validate(flat, self.param_specs())
+        eng = ClipEngine(self.config(), flat, device, self.is_bf16)
+        self._engines[key] = (p, eng)
+        return eng
+
+    def apply(self, variables, inputs=None, text_token_ids=None, text_paddings=None,
+              train: bool = False, normalize: bool = True,
+              return_intermediate: bool | Collection[str] = False, frame_paddings=None, **kwargs):
+        """encoders.py:788-910 -> (video_embeddings [B, D] | None, text_embeddings [B, D] | None,
+        outputs).  Embeddings are returned in the fprop dtype (encoders.py:50-67 casts the
+        normalised fp32 vector back)."""
+        del train
+        if kwargs.get("method") not in (None,):
+            raise NotImplementedError("apply(method=...) is not supported")
+        torch = _torch()
+        as_numpy = not any(isinstance(t, torch.Tensor) for t in (inputs, text_token_ids)
+                           if t is not None)
+        device = torch.cuda.current_device()
+        for t in (inputs, text_token_ids):
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                device = t.device.index
+        eng = self.engine(variables, device)
+        dev = f"cuda:{device}"
+        fdt = torch.bfloat16 if self.is_bf16 else torch.float32
+        video_emb = text_emb = None
+        outputs = {}
+        if inputs is not None:
+            x = inputs if isinstance(inputs, torch.Tensor) else torch.from_numpy(
+                np.ascontiguousarray(np.asarray(inputs, dtype=np.float32)))
+            x = x.to(dev)
+            if x.dim() != 5:
+                raise ValueError(f"inputs must be [B, T, H, W, 3], got {tuple(x.shape)}")
+            assert x.shape[2] == x.shape[3]  # encoders.py:435
+            if self.is_bf16 and x.dtype == torch.float32:
+                x = x.to(torch.bfloat16)
+            fp = None
+            if frame_paddings is not None:
+                fp = frame_paddings if isinstance(frame_paddings, torch.Tensor) else \
+                    torch.from_numpy(np.asarray(frame_paddings, dtype=np.float32))
+            vemb, femb, sp, st = eng.encode_video(
+                x, fp, normalize, want_frames=_contains(return_intermediate, "frame_embeddings"),
+                want_spatial=_contains(return_intermediate, "spatial_features"),
+                want_spatiotemporal=_contains(return_intermediate, "spatiotemporal_features"))
+            video_emb = vemb.to(fdt)
+            for k, v in (("spatial_features", sp), ("spatiotemporal_features", st),
+                         ("frame_embeddings", femb)):
+                if v is not None:
+                    outputs[k] = v.to(fdt)
+        if text_token_ids is not None:
+            assert text_paddings is not None, "Text paddings are required."
+            ids = text_token_ids if isinstance(text_token_ids, torch.Tensor) else \
+                torch.from_numpy(np.asarray(text_token_ids, dtype=np.int32))
+            pads = text_paddings if isinstance(text_paddings, torch.Tensor) else \
+                torch.from_numpy(np.asarray(text_paddings, dtype=np.float32))
+            text_emb = eng.encode_text(ids.to(dev), pads.to(dev), normalize).to(fdt)
+        if as_numpy:
+            cvt = lambda t: None if t is None else t.float().cpu().numpy()  # noqa: E731
+            video_emb, text_emb = cvt(video_emb), cvt(text_emb)
+            outputs = {k: cvt(v) for k, v in outputs.items()}
+        return video_emb, text_emb, outputs
 
     __call__ = apply

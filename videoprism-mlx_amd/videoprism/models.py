@@ -6,9 +6,11 @@ Same names and behaviour as the reference (models.py:54-336): `CONFIGS`, `MODELS
 runs its forward on MI355X through libvideoprism_hip.so.
 
 Differences, all forced by the offline deployment: `load_pretrained_weights` needs a
-local `checkpoint_path` (or a path in `checkpoints`) instead of a Hugging Face download;
-LvT (video-text) models are registered but their apply raises NotImplementedError until
-the text tower lands.
+local `checkpoint_path` (or a path in `checkpoints`) instead of a Hugging Face download.
+LvT (video-text) models return `encoders.FactorizedVideoCLIP` (encoders.py:762-910), whose
+`apply(variables, inputs, text_token_ids, text_paddings, ...)` runs both towers on MI355X;
+text tokenisation itself (tokenizers.py, sentencepiece model download) is out of scope, so
+callers pass token ids.
 """
 
 from __future__ import annotations
@@ -74,31 +76,16 @@ def videoprism_v1_giant():
     return encoders.FactorizedEncoder(**CONFIGS["videoprism_v1_giant"])
 
 
-class _PendingVideoCLIP:
-    """Placeholder for FactorizedVideoCLIP (encoders.py:762-910): registered so that
-    has_model/get_model behave like the reference; apply is not available yet."""
-
-    def __init__(self, **config):
-        self.config = config
-        self.fprop_dtype = None
-
-    def apply(self, *args, **kwargs):
-        raise NotImplementedError("LvT video-text models are not implemented on MI355X yet "
-                                  "(SURVEY.md §8(f) f1)")
-
-    init = apply
-
-
 def videoprism_lvt_v1_base(text_tokenizer: str = "c4_en"):
     config = dict(CONFIGS["videoprism_lvt_v1_base"])
     config["vocabulary_size"] = TEXT_TOKENIZERS[text_tokenizer]["vocab_size"]
-    return _PendingVideoCLIP(**config)
+    return encoders.FactorizedVideoCLIP(**config)
 
 
 def videoprism_lvt_v1_large(text_tokenizer: str = "c4_en"):
     config = dict(CONFIGS["videoprism_lvt_v1_large"])
     config["vocabulary_size"] = TEXT_TOKENIZERS[text_tokenizer]["vocab_size"]
-    return _PendingVideoCLIP(**config)
+    return encoders.FactorizedVideoCLIP(**config)
 
 
 MODELS = {

@@ -105,11 +105,33 @@ def load_video_encoder(model_name: str, weights_path: str = None, fprop_dtype=No
                         fprop_dtype=fprop_dtype)
 
 
-def load_model(model_name: str, weights_path: str = None):
-    """models_mlx.py:91-143 (video-text CLIP): not yet available on MI355X."""
-    get_model_config(model_name)
-    raise NotImplementedError("LvT video-text models are not implemented on MI355X yet "
-                              "(SURVEY.md §8(f) f1)")
+class VideoCLIP:
+    """Callable wrapper of the LvT model (encoders_mlx.py:826-910 call signature):
+    `model(inputs=None, text_token_ids=None, text_paddings=None, normalize=True,
+    return_intermediate=False, frame_paddings=None) -> (video_emb, text_emb, outputs)`."""
+
+    def __init__(self, config: dict, variables: dict, fprop_dtype=None):
+        cfg = {k: v for k, v in config.items()}
+        self.model = encoders.FactorizedVideoCLIP(fprop_dtype=fprop_dtype, **cfg)
+        self.variables = variables
+
+    def __call__(self, inputs=None, text_token_ids=None, text_paddings=None, normalize=True,
+                 return_intermediate=False, frame_paddings=None):
+        return self.model.apply(self.variables, inputs, text_token_ids, text_paddings,
+                                train=False, normalize=normalize,
+                                return_intermediate=return_intermediate,
+                                frame_paddings=frame_paddings)
+
+
+def load_model(model_name: str, weights_path: str = None, fprop_dtype=None) -> VideoCLIP:
+    """models_mlx.py:91-143: the LvT video-text model from a local weights file (a Flax
+    "repeated" npz of the full model, or unstacked `layers/{i}` keys)."""
+    config = get_model_config(model_name)
+    path = _resolve(model_name, weights_path)
+    flat = load_weights_from_file(str(path))
+    canonical = params_lib.canonical_params(flat)
+    return VideoCLIP(config, {"params": utils.recover_tree(list(canonical), list(canonical.values()))},
+                     fprop_dtype=fprop_dtype)
 
 
 def load_classifier(model_name: str, num_classes: int, weights_path: str = None):

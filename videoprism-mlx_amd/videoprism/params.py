@@ -67,6 +67,52 @@ def encoder_leaf_specs(cfg: dict, scan: bool = True) -> dict[str, tuple[int, ...
     return specs
 
 
+def _stack_specs(prefix: str, L: int, dims: dict, scan: bool) -> dict:
+    out = {}
+    for name, shp in _LAYER_LEAVES:
+        shape = tuple(dims[s] for s in shp)
+        if scan:
+            out[f"{prefix}/x_layers/{name}"] = (L,) + shape
+        else:
+            for i in range(L):
+                out[f"{prefix}/x_layers_{i}/{name}"] = shape
+    return out
+
+
+def clip_leaf_specs(cfg: dict, scan: bool = True) -> dict[str, tuple[int, ...]]:
+    """Flat {path: shape} of a FactorizedVideoCLIP (encoders.py:762-910) for a CONFIGS
+    'videoprism_lvt_*' entry plus `vocabulary_size`: the vision encoder under
+    'vision_encoder/', the auxiliary ViT (:846-857), the contrastive pooler
+    (layers.py:1044-1136, hidden 4D so dim_per_head = 4D/N) and the text tower
+    (:656-759, mlp_dim = 4D, :895).  88 leaves scanned / 136 unrolled for the reference's
+    tiny test config (encoders_test.py:339)."""
+    D = cfg["model_dim"]
+    nh = cfg["num_heads"]
+    specs = {f"vision_encoder/{k}": v for k, v in encoder_leaf_specs(cfg, scan).items()}
+    La = cfg.get("num_auxiliary_layers", 0)
+    if La > 0:
+        specs.update(_stack_specs("auxiliary_encoder/transformers_stack", La,
+                                  {"D": D, "N": nh, "H": D // nh, "F": cfg["mlp_dim"]}, scan))
+    dp = 4 * D // nh
+    pre = "contrastive_vision_pooler"
+    specs[f"{pre}/pooling_attention_query"] = (1, D)
+    specs[f"{pre}/pooling_attention/per_dim_scale/per_dim_scale"] = (dp,)
+    for q in ("query", "key", "value"):
+        specs[f"{pre}/pooling_attention/{q}/w"] = (D, nh, dp)
+        specs[f"{pre}/pooling_attention/{q}/b"] = (nh, dp)
+    specs[f"{pre}/pooling_attention/post/w"] = (D, nh, dp)
+    specs[f"{pre}/pooling_attention/post/b"] = (D,)
+    specs[f"{pre}/pooling_attention_layer_norm/scale"] = (D,)
+    specs[f"{pre}/pooling_attention_layer_norm/bias"] = (D,)
+    specs["text_encoder/token_emb/emb_var"] = (cfg["vocabulary_size"], D)
+    specs["text_encoder/cls_emb"] = (1, 1, D)
+    specs.update(_stack_specs("text_encoder/unimodal_transformer", cfg["num_unimodal_layers"],
+                              {"D": D, "N": nh, "H": D // nh, "F": 4 * D}, scan))
+    specs["text_encoder/unimodal_ln/scale"] = (D,)
+    specs["text_encoder/unimodal_ln/bias"] = (D,)
+    return specs
+
+
 def count_params(specs: dict[str, tuple[int, ...]]) -> int:
     return int(sum(int(np.prod(s)) for s in specs.values()))
 
@@ -170,22 +216,26 @@ def validate(flat: dict, specs: dict) -> None:
 # ------------------------------------------------------------------------------------ #
 # initialisers
 # ------------------------------------------------------------------------------------ #
-def synthetic_params(cfg: dict, seed: int = 0) -> dict:
+def synthetic_params(cfg: dict, seed: int = 0, specs: dict | None = None) -> dict:
     """Deterministic synthetic weights: kernels N(0, 1/fan_in), biases
     N(0, 0.02), LN scale N(0, 0.1) (used as 1+scale), positional embeddings N(0, 1/D).
     Non-zero biases/scales so that parity tests exercise every term.  Returns {'params': tree}."""
     rng = np.random.default_rng(seed)
     D = cfg["model_dim"]
     flat = {}
-    for k, shape in encoder_leaf_specs(cfg).items():
+    for k, shape in (specs or encoder_leaf_specs(cfg)).items():
         leaf = k.rsplit("/", 1)[-1]
-        if leaf in ("kernel", "w"):
+        if leaf == "pooling_attention_query":
+            std = 1.0
+        elif leaf == "cls_emb":
+            std = 1.0 / math.sqrt(D)
+        elif leaf in ("kernel", "w"):
             if k.endswith("post/w"):
                 fan_in = shape[-2] * shape[-1]
             else:
                 fan_in = shape[-3] if len(shape) >= 3 and k.endswith("/w") else shape[-2]
             std = 1.0 / math.sqrt(fan_in)
-        elif leaf == "scale":
+        elif leaf in ("scale", "per_dim_scale"):
             std = 0.1
         elif leaf == "emb_var":
             std = 1.0 / math.sqrt(D)
