@@ -10,7 +10,7 @@
 //   z[g,h,:]   = sum_s p[g,h,s] x[g,s,:]
 // which turns the two [S x D] x [D x 4D] projections per clip into two streaming passes over x
 // (HBM-bound: pool_logits, pool_wsum) and [G x D] x [D x dh] matrix products (small_gemm).
-//   pool_logits : logits[g][h][s] = x[g*S+s] . U[h]       (U staged in LDS, one wave per row)
+//   pool_logits : logits[g][h][s] = x[g*S+s] . U[h]       (bf16: skinny MFMA GEMM; fp32: U in LDS)
 //   pool_stats  : (max, 1/sum exp(l - max)) per (g, h)    (fp32 softmax, layers.py:650-654)
 //   pool_wsum   : zpart[g][c][h][:] = sum over the c-th 256-row chunk of p * x
 //   pool_reduce : z[g][h][:] = sum_c zpart
@@ -89,6 +89,46 @@ __global__ __launch_bounds__(256) void pool_logits_kernel(const void* __restrict
   }
 }
 
+// bf16 tokens: logits as a skinny GEMM on v_mfma_f32_32x32x16_bf16.  One wave owns 32 rows;
+// the B operand is Ut [32][D] bf16 = (U_hi | U_lo | 0) with U = U_hi + U_lo split on the host, so
+// the fp32 U survives the bf16 operands to ~2^-16 relative; lane c < H adds column H + c.
+__global__ __launch_bounds__(256) void pool_logits_mfma_kernel(const bf16_t* __restrict__ x, int64_t rows, int S,
+                                                               int D, const bf16_t* __restrict__ Ut, int H,
+                                                               float* __restrict__ logits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 32;
+  if (r0 >= rows) return;  // whole wave
+  const int i = lane & 31, half = lane >> 5;
+  const bf16_t* ap = x + (r0 + i) * D + 8 * half;
+  const bf16_t* bp = Ut + (int64_t)i * D + 8 * half;
+  f32x16 acc = {};
+  const int nt = D >> 4;
+  int t = 0;
+  for (; t + 8 <= nt; t += 8) {
+    bf16x8 a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a[u] = *reinterpret_cast<const bf16x8*>(ap + 16 * (t + u));
+      b[u] = *reinterpret_cast<const bf16x8*>(bp + 16 * (t + u));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], b[u], acc, 0, 0, 0);
+  }
+  for (; t < nt; ++t) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(ap + 16 * t);
+    const bf16x8 b = *reinterpret_cast<const bf16x8*>(bp + 16 * t);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+  // acc[r] = C[row = (r&3) + 8(r>>2) + 4*half][col = i]
+  const int64_t g = r0 / S;
+  const int64_t s0 = r0 % S;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float v = acc[r] + __shfl_down(acc[r], H);
+    if (i < H) logits[(g * H + i) * S + s0 + (r & 3) + 8 * (r >> 2) + 4 * half] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void pool_stats_kernel(const float* __restrict__ logits, int S,
                                                          float* __restrict__ stats) {
   __shared__ float red[4];
@@ -108,52 +148,60 @@ __global__ __launch_bounds__(256) void pool_stats_kernel(const float* __restrict
 constexpr int kPwRows = 256;  // rows per chunk
 constexpr int kPwMaxH = 16;
 
+// zpart[g][c][h][d] = sum over rows of chunk c of p[g,h,s] x[g*S+s][d]: a workgroup owns one
+// (g, 256-row chunk, 256-column quarter); a thread owns one column and all 16 head sums, the
+// probabilities of the chunk sit in LDS (float4 broadcast reads)
 __global__ __launch_bounds__(256) void pool_wsum_kernel(const void* __restrict__ x, int in_bf16, int S, int D,
                                                         int H, const float* __restrict__ logits,
                                                         const float* __restrict__ stats, int C,
                                                         float* __restrict__ zpart) {
-  __shared__ float ps[kPwRows][kPwMaxH];
-  const int g = blockIdx.x / C;
-  const int c = blockIdx.x % C;
+  __shared__ __attribute__((aligned(16))) float ps[kPwRows][kPwMaxH];
+  const int nq = D >> 8;
+  const int q = blockIdx.x % nq;
+  const int gc = blockIdx.x / nq;
+  const int g = gc / C;
+  const int c = gc % C;
   const int r0 = c * kPwRows;
   const int nr = S - r0 < kPwRows ? S - r0 : kPwRows;
-  for (int i = threadIdx.x; i < kPwRows * H; i += 256) {
-    const int r = i / H, h = i % H;
+  for (int i = threadIdx.x; i < kPwRows * kPwMaxH; i += 256) {
+    const int r = i / kPwMaxH, h = i % kPwMaxH;
     float p = 0.0f;
-    if (r < nr) {
+    if (r < nr && h < H) {
       const int64_t gh = (int64_t)g * H + h;
-      p = expf(logits[gh * S + r0 + r] - stats[2 * gh]) * stats[2 * gh + 1];
+      p = __expf(logits[gh * S + r0 + r] - stats[2 * gh]) * stats[2 * gh + 1];
     }
     ps[r][h] = p;
   }
   __syncthreads();
-  const int nj = D >> 8;  // columns per thread (D % 256 == 0, D <= 1024)
-  float acc[kPwMaxH][4];
+  const int d = q * 256 + threadIdx.x;
+  float acc[kPwMaxH];
 #pragma unroll
-  for (int h = 0; h < kPwMaxH; ++h)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[h][j] = 0.0f;
+  for (int h = 0; h < kPwMaxH; ++h) acc[h] = 0.0f;
   const int64_t rowbase = (int64_t)g * S + r0;
-  for (int r = 0; r < nr; ++r) {
-    float xv[4];
+  auto row = [&](int r, float xv) {
+    const float4* pr = reinterpret_cast<const float4*>(ps[r]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) xv[j] = j < nj ? ldx(x, in_bf16, (rowbase + r) * D + threadIdx.x + 256 * j) : 0.0f;
-#pragma unroll
-    for (int h = 0; h < kPwMaxH; ++h) {
-      if (h < H) {
-        const float p = ps[r][h];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[h][j] = fmaf(p, xv[j], acc[h][j]);
-      }
+    for (int h4 = 0; h4 < kPwMaxH / 4; ++h4) {
+      const float4 p = pr[h4];
+      acc[4 * h4] = fmaf(p.x, xv, acc[4 * h4]);
+      acc[4 * h4 + 1] = fmaf(p.y, xv, acc[4 * h4 + 1]);
+      acc[4 * h4 + 2] = fmaf(p.z, xv, acc[4 * h4 + 2]);
+      acc[4 * h4 + 3] = fmaf(p.w, xv, acc[4 * h4 + 3]);
     }
+  };
+  int r = 0;
+  for (; r + 8 <= nr; r += 8) {
+    float xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = ldx(x, in_bf16, (rowbase + r + u) * D + d);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) row(r + u, xv[u]);
   }
-  float* zp = zpart + ((int64_t)g * C + c) * H * D;
+  for (; r < nr; ++r) row(r, ldx(x, in_bf16, (rowbase + r) * D + d));
+  float* zp = zpart + ((int64_t)g * C + c) * H * D + d;
 #pragma unroll
   for (int h = 0; h < kPwMaxH; ++h)
-    if (h < H)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < nj) zp[(int64_t)h * D + threadIdx.x + 256 * j] = acc[h][j];
+    if (h < H) zp[(int64_t)h * D] = acc[h];
 }
 
 __global__ __launch_bounds__(256) void pool_reduce_kernel(const float* __restrict__ zpart, int C, int64_t HD,
@@ -167,21 +215,28 @@ __global__ __launch_bounds__(256) void pool_reduce_kernel(const float* __restric
   z[i] = s;
 }
 
-constexpr int kSgM = 8;
-constexpr int kSgK = 256;
+// out[m][n] = A[m][:] . Wt[:][n] + bias[n] for small M (pooled vectors): a workgroup owns 64
+// columns x 32 rows and splits K four ways (one quarter per wave, partial sums combined through
+// LDS); A^T chunks are staged in LDS and read as float4 broadcasts, Wt rows are coalesced.
+constexpr int kSgM = 32;
+constexpr int kSgN = 64;
+constexpr int kSgK = 128;
 
 __global__ __launch_bounds__(256) void small_gemm_kernel(const float* __restrict__ A, int64_t lda, int64_t sA,
                                                          const float* __restrict__ Wt, int64_t sW,
                                                          const float* __restrict__ bias, int64_t sB,
                                                          float* __restrict__ out, int64_t ldo, int64_t sO, int M,
                                                          int N, int K) {
-  __shared__ float As[kSgM][kSgK];
+  __shared__ __attribute__((aligned(16))) float At[kSgK][kSgM];  // A^T chunk
+  __shared__ float red[3][kSgM][kSgN];
   const int bz = blockIdx.z;
   A += bz * sA;
   Wt += bz * sW;
   out += bz * sO;
   const float* bb = bias ? bias + bz * sB : nullptr;
-  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int col = threadIdx.x & 63;
+  const int quarter = threadIdx.x >> 6;  // wave
+  const int n = blockIdx.x * kSgN + col;
   const int m0 = blockIdx.y * kSgM;
   float acc[kSgM];
 #pragma unroll
@@ -190,23 +245,36 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const float* __restrict
     __syncthreads();
     for (int i = threadIdx.x; i < kSgM * kSgK; i += 256) {
       const int mi = i / kSgK, kk = i % kSgK;
-      As[mi][kk] = (m0 + mi < M && k0 + kk < K) ? A[(int64_t)(m0 + mi) * lda + k0 + kk] : 0.0f;
+      At[kk][mi] = (m0 + mi < M && k0 + kk < K) ? A[(int64_t)(m0 + mi) * lda + k0 + kk] : 0.0f;
     }
     __syncthreads();
     if (n < N) {
-      const int kn = K - k0 < kSgK ? K - k0 : kSgK;
-      for (int kk = 0; kk < kn; ++kk) {
-        const float w = Wt[(int64_t)(k0 + kk) * N + n];
+      const int kq0 = quarter * (kSgK / 4);
+#pragma unroll 4
+      for (int kk = kq0; kk < kq0 + kSgK / 4; ++kk) {
+        const float w = k0 + kk < K ? Wt[(int64_t)(k0 + kk) * N + n] : 0.0f;
+        const float4* ar = reinterpret_cast<const float4*>(At[kk]);
 #pragma unroll
-        for (int i = 0; i < kSgM; ++i) acc[i] = fmaf(As[i][kk], w, acc[i]);
+        for (int i4 = 0; i4 < kSgM / 4; ++i4) {
+          const float4 a = ar[i4];
+          acc[4 * i4] = fmaf(a.x, w, acc[4 * i4]);
+          acc[4 * i4 + 1] = fmaf(a.y, w, acc[4 * i4 + 1]);
+          acc[4 * i4 + 2] = fmaf(a.z, w, acc[4 * i4 + 2]);
+          acc[4 * i4 + 3] = fmaf(a.w, w, acc[4 * i4 + 3]);
+        }
       }
     }
   }
-  if (n >= N) return;
+  if (quarter > 0) {
+#pragma unroll
+    for (int i = 0; i < kSgM; ++i) red[quarter - 1][i][col] = acc[i];
+  }
+  __syncthreads();
+  if (quarter > 0 || n >= N) return;
   const float b = bb ? bb[n] : 0.0f;
 #pragma unroll
   for (int i = 0; i < kSgM; ++i)
-    if (m0 + i < M) out[(int64_t)(m0 + i) * ldo + n] = acc[i] + b;
+    if (m0 + i < M) out[(int64_t)(m0 + i) * ldo + n] = acc[i] + red[0][i][col] + red[1][i][col] + red[2][i][col] + b;
 }
 
 __global__ __launch_bounds__(256) void ln_l2_rows_kernel(const void* __restrict__ x, int in_bf16, int64_t stride,
@@ -292,9 +360,15 @@ __global__ __launch_bounds__(256) void similarity_kernel(const float* __restrict
 
 }  // namespace
 
-hipError_t pool_logits(const void* x, int in_bf16, int64_t rows, int S, int D, const float* U, int H,
-                       float* logits, hipStream_t s) {
+hipError_t pool_logits(const void* x, int in_bf16, int64_t rows, int S, int D, const float* U, const bf16_t* Ut,
+                       int H, float* logits, hipStream_t s) {
   if (D % 64 || D > 1024 || H < 1 || H > kPwMaxH || rows % S) return hipErrorInvalidValue;
+  if (in_bf16 && Ut && S % 32 == 0) {
+    const int64_t grid = (rows / 32 + 3) / 4;
+    hipLaunchKernelGGL(pool_logits_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)x, rows, S,
+                       D, Ut, H, logits);
+    return hipGetLastError();
+  }
   const int64_t grid = (rows + kPlRows - 1) / kPlRows;
   hipLaunchKernelGGL(pool_logits_kernel, dim3((unsigned)grid), dim3(256), (size_t)H * D * 4, s, x, in_bf16, rows,
                      S, D, U, H, logits);
@@ -308,7 +382,8 @@ hipError_t pool_softmax_wsum(const void* x, int in_bf16, int G, int S, int D, in
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int C = (S + kPwRows - 1) / kPwRows;
-  hipLaunchKernelGGL(pool_wsum_kernel, dim3(G * C), dim3(256), 0, s, x, in_bf16, S, D, H, logits, stats, C, zpart);
+  hipLaunchKernelGGL(pool_wsum_kernel, dim3(G * C * (D / 256)), dim3(256), 0, s, x, in_bf16, S, D, H, logits, stats,
+                     C, zpart);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int64_t HD = (int64_t)H * D, total = (int64_t)G * HD;
@@ -323,7 +398,7 @@ hipError_t small_gemm(const float* A, int64_t lda, int64_t sA, const float* Wt, 
                       int64_t sB, float* out, int64_t ldo, int64_t sO, int M, int N, int K, int batch,
                       hipStream_t s) {
   if (M < 1 || N < 1 || K < 1 || batch < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(small_gemm_kernel, dim3((N + 255) / 256, (M + kSgM - 1) / kSgM, batch), dim3(256), 0, s, A,
+  hipLaunchKernelGGL(small_gemm_kernel, dim3((N + kSgN - 1) / kSgN, (M + kSgM - 1) / kSgM, batch), dim3(256), 0, s, A,
                      lda, sA, Wt, sW, bias, sB, out, ldo, sO, M, N, K);
   return hipGetLastError();
 }

@@ -26,6 +26,7 @@ struct vp_clip {
   bool bf16() const { return cfg.video.fprop_dtype == VP_BF16; }
   std::vector<vpi::LayerW> aux, text;
   // contrastive pooler (fp32): U [H][D], Wv^T [H][D][dp], bv [H][dp], Wpost^T [H*dp][D], bpost [D]
+  void* pUt = nullptr;  // [32][D] bf16: U_hi rows 0..H-1, U_lo rows H..2H-1, zeros
   float *pU = nullptr, *pWvT = nullptr, *pbv = nullptr, *pWpT = nullptr, *pbp = nullptr;
   float *pln_g = nullptr, *pln_b = nullptr;
   // text tower: token table [V][D] (fprop dtype), cls [D], sinusoidal table [kMaxTextLen][D]
@@ -140,7 +141,21 @@ int pack_pooler(vp_clip* c) {
   std::vector<float> g(D);
   const auto& sc = param_data(c, "contrastive_vision_pooler/pooling_attention_layer_norm/scale");
   for (int64_t d = 0; d < D; ++d) g[d] = sc[d] + 1.0f;
+  // bf16 hi/lo split of U for the MFMA logits kernel
+  std::vector<uint16_t> ut((size_t)32 * D, 0);
+  for (int64_t h = 0; h < H; ++h)
+    for (int64_t d = 0; d < D; ++d) {
+      const float u = U[(size_t)h * D + d];
+      const uint16_t hi = host_f2bf(u);
+      uint32_t hb = (uint32_t)hi << 16;
+      float hf;
+      std::memcpy(&hf, &hb, 4);
+      ut[(size_t)h * D + d] = hi;
+      ut[(size_t)(H + h) * D + d] = host_f2bf(u - hf);
+    }
   int rc;
+  if ((rc = dev_alloc(c, ut.size() * 2, &c->pUt))) return rc;
+  VP_HIP(hipMemcpy(c->pUt, ut.data(), ut.size() * 2, hipMemcpyHostToDevice));
   if ((rc = upload_f32(c, U, &c->pU)) || (rc = upload_f32(c, wvt, &c->pWvT)) || (rc = upload_f32(c, bv, &c->pbv)) ||
       (rc = upload_f32(c, wpt, &c->pWpT)) || (rc = upload_f32(c, bp, &c->pbp)) || (rc = upload_f32(c, g, &c->pln_g)) ||
       (rc = upload_f32(c, param_data(c, "contrastive_vision_pooler/pooling_attention_layer_norm/bias"), &c->pln_b)))
@@ -349,7 +364,7 @@ int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B,
   auto pool = [&](int G, int Sg, float* dst) -> int {
     const double bytes = 2.0 * M * D * es;  // two streaming passes over the tokens
     VP_HIP(f.rec(PC_POOL, 2.0 * 2.0 * M * D * NH, bytes, [&] {
-      hipError_t e = pool_logits(feat, bf, M, Sg, D, c->pU, NH, logits, s);
+      hipError_t e = pool_logits(feat, bf, M, Sg, D, c->pU, (const bf16_t*)c->pUt, NH, logits, s);
       if (e != hipSuccess) return e;
       return pool_softmax_wsum(feat, bf, G, Sg, D, NH, logits, stats, zpart, z, s); }));
     VP_HIP(small_gemm(z, (int64_t)NH * D, D, c->pWvT, (int64_t)D * dp, c->pbv, dp, enc, (int64_t)NH * dp, dp, G, dp,

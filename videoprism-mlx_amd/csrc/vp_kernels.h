@@ -123,8 +123,9 @@ hipError_t attention_masked(const void* qkv, void* o, int in_is_bf16, int num_se
                             float cap, const float* key_pad, int causal, hipStream_t s);
 // contrastive pooler: logits[g][h][s] = x[g*S+s] . U[h]; then softmax per (g,h) and
 // z[g][h][:] = sum_s p x (zpart scratch: [G][pool_chunks(S)][H][D], stats [G*H][2])
-hipError_t pool_logits(const void* x, int in_bf16, int64_t rows, int S, int D, const float* U, int H,
-                       float* logits, hipStream_t s);
+// (bf16 x with Ut = [32][D] bf16 (U_hi | U_lo | 0) and S % 32 == 0: MFMA kernel)
+hipError_t pool_logits(const void* x, int in_bf16, int64_t rows, int S, int D, const float* U, const bf16_t* Ut,
+                       int H, float* logits, hipStream_t s);
 hipError_t pool_softmax_wsum(const void* x, int in_bf16, int G, int S, int D, int H, const float* logits,
                              float* stats, float* zpart, float* z, hipStream_t s);
 int pool_chunks(int S);
