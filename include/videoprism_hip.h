@@ -47,7 +47,9 @@ enum vp_status {
   VP_ENOTSUP = 5,  /* valid for the reference but outside this library's kernels */
 };
 
-enum vp_dtype { VP_F32 = 0, VP_BF16 = 1 };
+/* VP_U8: video frames as uint8 [0, 255], normalised in the patchify kernel exactly as
+ * video_utils.py:94 (float32(v) / 255.0) -- a quarter of the fp32 input bytes. */
+enum vp_dtype { VP_F32 = 0, VP_BF16 = 1, VP_U8 = 2 };
 
 /* FactorizedEncoder hyper-parameters: models.py:83-104 CONFIGS / encoders.py:399-408. */
 typedef struct vp_config {
@@ -85,12 +87,18 @@ int vp_param_name(const vp_handle* h, int index, const char** name);
 /* Validates that every leaf was set and uploads the packed weights (one-off). */
 int vp_finalize(vp_handle* h);
 
+/* Frames whose patch grid (H/P, W/P) differs from pos_emb_shape[1:]: interpolates the spatial
+ * positional table the way encoders.py:497-512 does (_interpolate_emb_2d, jax.image.resize
+ * 'bilinear', antialiased when shrinking) and caches it on the device (allocates; call once per
+ * new frame size before vp_forward, which never allocates). */
+int vp_prepare_geometry(vp_handle* h, int64_t H, int64_t W);
+
 /* Workspace needed by vp_forward for inputs [B, T, H, W, 3]. */
 int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W,
                        size_t* bytes);
 
 /* Replaces FactorizedEncoder.__call__ (encoders.py:411-456) / model.apply(..., train=False).
- *   video          device [B, T, H, W, 3], in_dtype VP_F32 or VP_BF16, values as given
+ *   video          device [B, T, H, W, 3], in_dtype VP_F32 or VP_BF16 (values as given) or VP_U8
  *   frame_paddings device [B, T] fp32 (1 = padded frame) or NULL (encoders.py:440-447)
  *   out            device [B, T*N, D] embeddings in out_dtype (token = t*N + n, :570-572)
  *   spatial_out    device [B, T*N, D] 'spatial_features' in out_dtype, or NULL (:574-578)

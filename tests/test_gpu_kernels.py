@@ -421,3 +421,21 @@ def test_gemm_row_stats(cuda, epi):
     ref = torch.stack([rstd, -mean * rstd], 1)
     assert torch.allclose(rs_p.double(), ref, rtol=2e-5, atol=1e-5)
     assert torch.allclose(rs_r.double(), ref, rtol=2e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("variant", [16, 32, 48])
+def test_attention_spatial_layout_variants(cuda, variant):
+    """Head-major q|k|v (bit 16) and LDS-staged O stores (bit 32) are bitwise equal to the
+    production spatial kernel on the same values."""
+    nseq, heads, S = 3, 12, 256
+    D = heads * 64
+    qkv = _bf(_qkv(nseq, S, heads, 5)).to(cuda)
+    ref = nat.op_attention(qkv, nseq, S, heads, 50.0)
+    src = qkv
+    if variant & 16:  # [M, 3, heads, 64] -> [3, heads, M, 64]
+        src = qkv.reshape(nseq * S, 3, heads, 64).permute(1, 2, 0, 3).contiguous()
+    out = torch.empty_like(ref)
+    nat.call("vp_dev_attention_diag", variant, src.data_ptr(), out.data_ptr(), nseq, heads, 50.0,
+             torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

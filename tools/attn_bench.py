@@ -34,6 +34,7 @@ def main():
     qkv = qkv.to(torch.bfloat16)
     o = torch.empty((nseq * S, D), device=dev, dtype=torch.bfloat16)
     st = lambda: torch.cuda.current_stream().cuda_stream
+    # 16: head-major q|k|v, 32: LDS-staged O stores (48: both), 1..3: ablations
     diags = [int(a) for a in sys.argv[1:]] or [0, 1, 2, 3]
     fns = {f"d{d}": (lambda d=d: nat.call("vp_dev_attention_diag", d, qkv.data_ptr(), o.data_ptr(), nseq,
                                           heads, 50.0, st())) for d in diags}

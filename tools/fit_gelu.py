@@ -1,0 +1,52 @@
+"""Fits the polynomial R(a) of the one-transcendental GELU epilogue:
+
+    Phi(-a) = exp(-a^2 / 2) * R(a),   a = |x| in [0, AMAX]
+    gelu(x) = x * Phi(x) = x >= 0 ? x - x*Phi(-a) : x*Phi(-a)
+
+R(a) = erfc(a/sqrt2)/2 * exp(a^2/2) is smooth and positive, so a low-degree polynomial reaches
+a relative error far below the bf16 output rounding (2^-9).  Weighted least squares iterated
+toward minimax on the relative error; prints the fp32-Horner error per degree and the
+coefficients of the chosen degree.   python tools/fit_gelu.py [degree]
+"""
+import sys
+
+import numpy as np
+from scipy.special import erfc
+
+AMAX = 5.5
+
+
+def fit(deg, a, R):
+    V = np.vander(a, deg + 1, increasing=True)
+    ww = 1.0 / R
+    for _ in range(40):
+        c, *_ = np.linalg.lstsq(V * ww[:, None], R * ww, rcond=None)
+        err = (V @ c - R) / R
+        ww = ww * (1.0 + np.abs(err) / np.abs(err).max()) ** 2
+    return c
+
+
+def horner32(c, a):
+    cf = c.astype(np.float32)
+    af = a.astype(np.float32)
+    p = np.full_like(af, cf[-1])
+    for k in range(len(cf) - 2, -1, -1):
+        p = p * af + cf[k]
+    return p.astype(np.float64)
+
+
+def main():
+    a = np.linspace(0.0, AMAX, 40001)
+    R = 0.5 * erfc(a / np.sqrt(2.0)) * np.exp(a * a / 2.0)
+    want = int(sys.argv[1]) if len(sys.argv) > 1 else None
+    for deg in range(5, 12):
+        c = fit(deg, a, R)
+        e32 = np.abs((horner32(c, a) - R) / R).max()
+        print(f"degree {deg}: max relative error (fp32 Horner) {e32:.3e}")
+        if deg == want:
+            print("coefficients (a^0 .. a^n):")
+            print(", ".join(f"{float(np.float32(v))!r}f" for v in c))
+
+
+if __name__ == "__main__":
+    main()

@@ -55,10 +55,13 @@ constexpr int kSpThreads = 512;
 constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 
 // DIAG (ablation builds, results garbage): 1 = no capped-exp VALU (p = logit), 2 = no P.V MFMAs
-template <bool MASK, int DIAG = 0>
+// q|k|v layout by strides (elements): row rs, head hs, section (q -> k -> v) sec; the row-major
+// fused projection output is (3D, 64, D), a head-major one (64, M*64, heads*M*64).
+// STAGE: O goes through LDS and leaves as whole 128-B row segments (8 rows per store).
+template <bool MASK, int DIAG = 0, bool STAGE = false>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
-    const float* __restrict__ key_pad, int rev) {
+    const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + kSpS * 128;
@@ -66,7 +69,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   int* allmask = reinterpret_cast<int*>(kp + kSpS);
 
   const int D = heads * 64;
-  const int64_t ld = 3 * (int64_t)D;
+  const int64_t ld = rs;
   // rev: sequences in reverse order, so the last-written (Infinity-Cache resident) q|k|v rows
   // of the producing GEMM are read first
   const int bid = rev ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   const int h = bid % heads;
   const int lane = threadIdx.x & 63;
   const int w = wave_id();
-  const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * 64;
+  const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * hs;
 
   // ---- this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j),
   // requested first by loads the compiler does not see (a visible load would make hipcc wait
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       const int piece = isV * 32 + cc * 8 + w;
       const int row = (piece & 31) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
-      const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * D : D) + c * 8;
+      const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * sec : sec) + c * 8;
       __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
     }
   if constexpr (MASK) {  // (padded batches: no streaming)
@@ -220,6 +223,31 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;
   // y_dh[i] = O^T[d = 32dh + (i&3) + 8(i>>2) + 4*half][q = q0 + (l&31)]
+  if constexpr (STAGE) {
+    // every wave is done with K/V: the wave's 32 x 64 output tile goes to its 4 KiB of the K
+    // region ([q][16-B chunk ^ (q & 7)]), then 8 lanes per row store whole 128-B segments
+    __syncthreads();
+    char* st = smem + w * 4096;
+    const int ql = lane & 31;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const uint2 v0 = make_uint2(pack_bf16x2(y0[4 * g4] * inv, y0[4 * g4 + 1] * inv),
+                                  pack_bf16x2(y0[4 * g4 + 2] * inv, y0[4 * g4 + 3] * inv));
+      const uint2 v1 = make_uint2(pack_bf16x2(y1[4 * g4] * inv, y1[4 * g4 + 1] * inv),
+                                  pack_bf16x2(y1[4 * g4 + 2] * inv, y1[4 * g4 + 3] * inv));
+      *reinterpret_cast<uint2*>(st + ql * 128 + (((g4) ^ (ql & 7)) << 4) + 8 * half) = v0;
+      *reinterpret_cast<uint2*>(st + ql * 128 + (((4 + g4) ^ (ql & 7)) << 4) + 8 * half) = v1;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int r = p * 8 + (lane >> 3), c = lane & 7;
+      const uint4 v = *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
+      *reinterpret_cast<uint4*>(o + ((int64_t)seq * kSpS + q0 + r) * D + h * 64 + c * 8) = v;
+    }
+    return;
+  }
   bf16_t* op = o + ((int64_t)seq * kSpS + q0 + (lane & 31)) * D + h * 64 + 4 * half;
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
@@ -406,7 +434,7 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   if (!(cap > 0.0f)) return hipErrorInvalidValue;
   static bool attr[2] = {false, false};
   const int mi = key_pad ? 1 : 0;
-  const void* fn = key_pad ? (const void*)attn_spatial_kernel<true> : (const void*)attn_spatial_kernel<false>;
+  const void* fn = key_pad ? (const void*)attn_spatial_kernel<true, 0, true> : (const void*)attn_spatial_kernel<false, 0, true>;
   if (!attr[mi]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
     if (e != hipSuccess) return e;
@@ -417,22 +445,35 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   // (a persistent variant -- one workgroup per CU walking (frame, head) pairs, next pair's
   // Q/K/V staged by LDS-DMA during the current one, 160 KiB LDS -- measured 255 vs 218 us: at
   // 2 waves per SIMD the softmax/P.V phase loses more than the continuous stream gains)
+  // O leaves through LDS as whole 128-B row segments (tools/attn_bench.py: 217 -> 209 us at the
+  // bench shape); a head-major q|k|v layout measured only 1 % faster and is not used
+  const int64_t D = heads * 64;
   if (key_pad)
-    hipLaunchKernelGGL(attn_spatial_kernel<true>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad, rev);
+    hipLaunchKernelGGL((attn_spatial_kernel<true, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
+                       key_pad, rev, 3 * D, (int64_t)64, D);
   else
-    hipLaunchKernelGGL(attn_spatial_kernel<false>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad, rev);
+    hipLaunchKernelGGL((attn_spatial_kernel<false, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
+                       key_pad, rev, 3 * D, (int64_t)64, D);
   return hipGetLastError();
 }
 
 hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, hipStream_t s) {
   const dim3 grid(num_seq * heads);
+  const int64_t D = heads * 64, M = (int64_t)num_seq * kSpS;
+  // diag >= 16: layout / store variants of the production kernel (bit 16: head-major q|k|v,
+  // bit 32: LDS-staged O stores)
+  const int64_t rs = (diag & 16) ? 64 : 3 * D, hs = (diag & 16) ? M * 64 : 64, sec = (diag & 16) ? heads * M * 64 : D;
   auto go = [&](const void* fn, auto kern) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, nullptr, 0);
+    hipLaunchKernelGGL(kern, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, nullptr, 0, rs, hs, sec);
     return hipGetLastError();
   };
+  if (diag >= 16) {
+    if (diag & 32) return go((const void*)attn_spatial_kernel<false, 0, true>, attn_spatial_kernel<false, 0, true>);
+    return go((const void*)attn_spatial_kernel<false, 0, false>, attn_spatial_kernel<false, 0, false>);
+  }
   switch (diag) {
     case 0: return go((const void*)attn_spatial_kernel<false, 0>, attn_spatial_kernel<false, 0>);
     case 1: return go((const void*)attn_spatial_kernel<false, 1>, attn_spatial_kernel<false, 1>);

@@ -34,7 +34,9 @@ __global__ __launch_bounds__(256) void patchify_kernel(const TI* __restrict__ vi
         const int p = k / (P * C);
         const int rem = k - p * P * C;  // = q*C + c, contiguous in the source row
         const int64_t off = (((int64_t)bt * H + mi * P + p) * W + ni * P) * C + rem;
-        if constexpr (sizeof(TI) == 2) x = bf2f(video[off]); else x = video[off];
+        if constexpr (sizeof(TI) == 1) x = (float)video[off] / 255.0f;  // video_utils.py:94
+        else if constexpr (sizeof(TI) == 2) x = bf2f(video[off]);
+        else x = video[off];
       }
       v[j] = x;
     }
@@ -310,26 +312,23 @@ hipError_t ln_launch(const void* x, int in_is_bf16, int rows, const float* gamma
 
 }  // namespace
 
-hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is_bf16, int BT, int H,
+hipError_t patchify(const void* video, int in_dtype, void* patches, int out_is_bf16, int BT, int H,
                     int W, int C, int P, int kpad, hipStream_t s) {
-  if (kpad % 8 || kpad < P * P * C || H % P || W % P) return hipErrorInvalidValue;
+  if (kpad % 8 || kpad < P * P * C || H % P || W % P || in_dtype < 0 || in_dtype > 2) return hipErrorInvalidValue;
   const int64_t work = (int64_t)BT * (H / P) * (W / P) * (kpad / 8);
   const int grid = grid_for(work, 256);
-  if (in_is_bf16) {
+  auto go = [&](auto in_tag) {
+    using TI = decltype(in_tag);
     if (out_is_bf16)
-      hipLaunchKernelGGL((patchify_kernel<bf16_t, bf16_t>), dim3(grid), dim3(256), 0, s,
-                         (const bf16_t*)video, (bf16_t*)patches, BT, H, W, C, P, kpad);
+      hipLaunchKernelGGL((patchify_kernel<TI, bf16_t>), dim3(grid), dim3(256), 0, s, (const TI*)video,
+                         (bf16_t*)patches, BT, H, W, C, P, kpad);
     else
-      hipLaunchKernelGGL((patchify_kernel<bf16_t, float>), dim3(grid), dim3(256), 0, s,
-                         (const bf16_t*)video, (float*)patches, BT, H, W, C, P, kpad);
-  } else {
-    if (out_is_bf16)
-      hipLaunchKernelGGL((patchify_kernel<float, bf16_t>), dim3(grid), dim3(256), 0, s,
-                         (const float*)video, (bf16_t*)patches, BT, H, W, C, P, kpad);
-    else
-      hipLaunchKernelGGL((patchify_kernel<float, float>), dim3(grid), dim3(256), 0, s,
-                         (const float*)video, (float*)patches, BT, H, W, C, P, kpad);
-  }
+      hipLaunchKernelGGL((patchify_kernel<TI, float>), dim3(grid), dim3(256), 0, s, (const TI*)video,
+                         (float*)patches, BT, H, W, C, P, kpad);
+  };
+  if (in_dtype == 1) go(bf16_t{});
+  else if (in_dtype == 2) go(uint8_t{});
+  else go(float{});
   return hipGetLastError();
 }
 

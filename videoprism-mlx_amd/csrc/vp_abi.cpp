@@ -116,6 +116,7 @@ int vp_finalize(vp_handle* h) {
     if ((rc = upload_f32(h, param_data(h, px + "patch_projection/linear/bias"), &h->bpatch))) return rc;
   }
   if ((rc = upload_f32(h, param_data(h, px + "spatial_pos_emb/emb_var"), &h->spatial_pos))) return rc;
+  h->spatial_pos_host = param_data(h, px + "spatial_pos_emb/emb_var");
   {  // temporal positional tables for every T in 1..kMaxT (encoders.py:543-553)
     const auto& e = param_data(h, px + "temporal_pos_emb/emb_var");
     const int Tp = c.pos_emb_t;
@@ -158,6 +159,46 @@ int vp_finalize(vp_handle* h) {
   return VP_OK;
 }
 
+int vp_prepare_geometry(vp_handle* h, int64_t H, int64_t W) {
+  if (!h) return fail(VP_EINVAL, "null handle");
+  if (!h->finalized) return fail(VP_ESTATE, "vp_finalize has not been called");
+  const vp_config& c = h->cfg;
+  const int64_t P = c.patch_size, D = c.model_dim;
+  if (H < 1 || W < 1 || H % P || W % P)
+    return fail(VP_EINVAL, "Image height (" + std::to_string(H) + ") and width (" + std::to_string(W) +
+                               ") should be multiples of patch_size (" + std::to_string(P) + ").");
+  const int gm = (int)(H / P), gn = (int)(W / P);
+  if ((gm == c.pos_emb_h && gn == c.pos_emb_w) || h->grid_pos.count({gm, gn})) return VP_OK;
+  // _interpolate_emb_2d (encoders.py:133-165): separable jax.image.resize 'bilinear' (antialiased
+  // when shrinking) of the [pos_h, pos_w, D] table, fp64 on the host
+  const int ph = c.pos_emb_h, pw = c.pos_emb_w;
+  const auto wh = resize_weights(ph, gm), ww = resize_weights(pw, gn);
+  const auto& e = h->spatial_pos_host;
+  std::vector<float> out((size_t)gm * gn * D);
+  std::vector<double> acc(D);
+  for (int i = 0; i < gm; ++i)
+    for (int j = 0; j < gn; ++j) {
+      std::fill(acc.begin(), acc.end(), 0.0);
+      for (int a = 0; a < ph; ++a) {
+        const double wa = wh[(size_t)a * gm + i];
+        if (wa == 0.0) continue;
+        for (int b = 0; b < pw; ++b) {
+          const double w = wa * ww[(size_t)b * gn + j];
+          if (w == 0.0) continue;
+          const float* src = e.data() + ((size_t)a * pw + b) * D;
+          for (int64_t d = 0; d < D; ++d) acc[d] += w * src[d];
+        }
+      }
+      for (int64_t d = 0; d < D; ++d) out[((size_t)i * gn + j) * D + d] = (float)acc[d];
+    }
+  VP_HIP(hipSetDevice(h->device));
+  float* dev = nullptr;
+  int rc = upload_f32(h, out, &dev);
+  if (rc) return rc;
+  h->grid_pos[{gm, gn}] = dev;
+  return VP_OK;
+}
+
 int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W,
                        size_t* bytes) {
   if (!h || !bytes) return fail(VP_EINVAL, "null argument");
@@ -173,7 +214,8 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   using namespace vp;
   if (!h || !video || !out || !workspace) return fail(VP_EINVAL, "null argument");
   if (!h->finalized) return fail(VP_ESTATE, "vp_finalize has not been called");
-  if ((in_dtype != VP_F32 && in_dtype != VP_BF16) || (out_dtype != VP_F32 && out_dtype != VP_BF16))
+  if ((in_dtype != VP_F32 && in_dtype != VP_BF16 && in_dtype != VP_U8) ||
+      (out_dtype != VP_F32 && out_dtype != VP_BF16))
     return fail(VP_EINVAL, "bad dtype");
   int rc = check_geometry(h, B, T, H, W);
   if (rc) return rc;
@@ -185,7 +227,15 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   const bool bf = is_bf16(h);
   const int P_ = c.patch_size;
   const int Nsp = (int)((H / P_) * (W / P_));
-  const int M = (int)(B * T * Nsp);
+  const int M = (int)(B * T * Nsp);  // tokens
+  const int Mp = (int)padded_rows(h, M);  // GEMM rows
+  const float* sp_pos = h->spatial_pos;
+  if (Nsp != c.pos_emb_h * c.pos_emb_w || H / P_ != c.pos_emb_h) {  // encoders.py:497-512
+    auto it = h->grid_pos.find({(int)(H / P_), (int)(W / P_)});
+    if (it == h->grid_pos.end())
+      return fail(VP_ESTATE, "patch grid differs from pos_emb_shape[1:]: call vp_prepare_geometry first");
+    sp_pos = it->second;
+  }
   const int D = c.model_dim, F = c.mlp_dim, NH = c.num_heads;
   const size_t es = bf ? 2 : 4;
   char* ws = static_cast<char*>(workspace);
@@ -198,20 +248,24 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   if (frame_paddings) {
     pad_btn = reinterpret_cast<float*>(ws + L.pad_btn);
     pad_bnt = reinterpret_cast<float*>(ws + L.pad_bnt);
+    if (Mp > M) {
+      VP_HIP(hipMemsetAsync(pad_btn + M, 0, (size_t)(Mp - M) * 4, s));
+      VP_HIP(hipMemsetAsync(pad_bnt + M, 0, (size_t)(Mp - M) * 4, s));
+    }
     VP_HIP(expand_paddings(frame_paddings, (int)B, (int)T, Nsp, pad_btn, pad_bnt, s));
   }
   // bf16: LayerNorms inside the layers are folded into the consuming GEMMs (EPI_*_LN); the
   // residual-stream producers emit row statistics (EPI_*_ST) that ln_stats_finalize turns into
   // (rstd, -mean*rstd) per row
   Fwd f;
-  f.s = s; f.bf = bf; f.M = M; f.D = D; f.NH = NH; f.cap = c.atten_logit_cap;
+  f.s = s; f.bf = bf; f.M = Mp; f.D = D; f.NH = NH; f.cap = c.atten_logit_cap;
   f.hb = hb; f.big = big;
   f.st_part = reinterpret_cast<float*>(ws + L.st_part);
   f.ln_rs = reinterpret_cast<float*>(ws + L.ln_rs);
   f.pf = &h->prof;
   float* ln_rs = f.ln_rs;
   const int epi_pos = bf ? EPI_POS_BF16 : EPI_POS_F32;
-  const char* ge = bf ? gemm_bf16_check(M, 3 * D, D, D, D) : gemm_f32_check(M, 3 * D, D);
+  const char* ge = bf ? gemm_bf16_check(Mp, 3 * D, D, D, D) : gemm_f32_check(Mp, 3 * D, D);
   if (ge) return fail(VP_ENOTSUP, ge);
   const double dM = M, dD = D, dE = (double)es;
   auto gbytes = [&](double K, double N, double outb, double resid) {  // algorithmic GEMM bytes
@@ -220,12 +274,15 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
 
   // 1. tokenisation + patch projection + spatial pos-emb (encoders.py:436-514)
   const double kreal = (double)P_ * P_ * 3;
-  VP_HIP(f.rec(PC_PATCHIFY, 0.0, dM * kreal * (in_dtype == VP_BF16 ? 2 : 4) + dM * h->kpad * dE, [&] {
-    return patchify(video, in_dtype == VP_BF16, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
+  const double in_es = in_dtype == VP_U8 ? 1 : in_dtype == VP_BF16 ? 2 : 4;
+  if (Mp > M) VP_HIP(hipMemsetAsync(static_cast<char*>(big) + (size_t)M * h->kpad * es, 0,
+                                    (size_t)(Mp - M) * h->kpad * es, s));
+  VP_HIP(f.rec(PC_PATCHIFY, 0.0, dM * kreal * in_es + dM * h->kpad * dE, [&] {
+    return patchify(video, in_dtype, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
   const bool fold = bf && c.num_spatial_layers > 0;  // LN1 of spatial layer 0 folded
   VP_HIP(f.rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, dE, 0), [&] {
     return f.gemm(fold ? EPI_POS_BF16_ST : epi_pos, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr,
-                  h->spatial_pos, Nsp, nullptr); }));
+                  sp_pos, Nsp, nullptr); }));
   const double ln_bytes = dM * dD * dE + dM * dD * dE;
   if (fold) VP_HIP(f.finalize());
   auto run_stack = [&](std::vector<LayerW>& layers, void* xs, int num_seq, int S, const float* pad) -> int {
@@ -475,7 +532,8 @@ int vp_op_patchify(const void* video, int in_dtype, void* patches, int out_dtype
     return fail(VP_EINVAL, "Image height (" + std::to_string(H) + ") and width (" + std::to_string(W) +
                                ") should be multiples of patch_size (" + std::to_string(P) + ").");
   if (kpad % 8 || kpad < P * P * C) return fail(VP_EINVAL, "kpad must be >= P*P*C and a multiple of 8");
-  VP_HIP(patchify(video, in_dtype == VP_BF16, patches, out_dtype == VP_BF16, (int)BT, (int)H, (int)W,
+  if (in_dtype != VP_F32 && in_dtype != VP_BF16 && in_dtype != VP_U8) return fail(VP_EINVAL, "bad dtype");
+  VP_HIP(patchify(video, in_dtype, patches, out_dtype == VP_BF16, (int)BT, (int)H, (int)W,
                   (int)C, (int)P, (int)kpad, static_cast<hipStream_t>(stream)));
   return VP_OK;
 }

@@ -323,7 +323,8 @@ int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B,
   const int64_t M64 = B * T * N;
   if (M64 > 0x7fffffff) return fail(VP_ENOTSUP, "too many tokens");
   const int M = (int)M64;
-  if (!bf && c->cfg.num_auxiliary_layers > 0 && M % 128) return fail(VP_ENOTSUP, "fp32 GEMM needs B*T*N % 128 == 0");
+  if (c->cfg.num_auxiliary_layers > 0 && M % (bf ? 256 : 128))
+    return fail(VP_ENOTSUP, "auxiliary encoder GEMMs need B*T*N % 256 == 0 (bf16) / 128 (fp32)");
   char* ws = static_cast<char*>(workspace);
   void* feat = ws + L.feat;
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -128,6 +128,8 @@ struct vp_handle {
   void* wpatch = nullptr;      // [D][kpad]
   float* bpatch = nullptr;
   float* spatial_pos = nullptr;    // [pos_h*pos_w][D]
+  std::vector<float> spatial_pos_host;                   // kept for other patch grids
+  std::map<std::pair<int, int>, float*> grid_pos;        // interpolated tables (vp_prepare_geometry)
   float* temporal_pos = nullptr;   // [kMaxT+1][kMaxT][D]: table for T at offset T*kMaxT*D
   std::vector<vpi::LayerW> spatial, temporal;
   float *sln_g = nullptr, *sln_b = nullptr, *tln_g = nullptr, *tln_b = nullptr;
@@ -334,10 +336,17 @@ struct WsLayout {
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// GEMM row count: B*T*N padded to the GEMM tile (256 rows bf16, 128 fp32); the padding rows
+// ride through the row-independent GEMM / LayerNorm kernels and are never read back
+inline int64_t padded_rows(const vp_handle* h, int64_t M) {
+  const int64_t t = is_bf16(h) ? 256 : 128;
+  return (M + t - 1) / t * t;
+}
+
 inline WsLayout ws_layout(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W) {
   const int64_t P = h->cfg.patch_size;
   const int64_t Nsp = (H / P) * (W / P);
-  const int64_t M = B * T * Nsp;
+  const int64_t M = padded_rows(h, B * T * Nsp);
   const int64_t D = h->cfg.model_dim, F = h->cfg.mlp_dim;
   const size_t es = is_bf16(h) ? 2 : 4;
   const int64_t kpad = ((P * P * 3 + 63) / 64) * 64;
@@ -366,14 +375,8 @@ inline int check_geometry(const vp_handle* h, int64_t B, int64_t T, int64_t H, i
   if (H % P || W % P)
     return fail(VP_EINVAL, "Image height (" + std::to_string(H) + ") and width (" + std::to_string(W) +
                                ") should be multiples of patch_size (" + std::to_string(P) + ").");
-  if (H / P != h->cfg.pos_emb_h || W / P != h->cfg.pos_emb_w)
-    return fail(VP_ENOTSUP, "patch grid must equal pos_emb_shape[1:] (no spatial interpolation yet)");
   if (T > kMaxT) return fail(VP_ENOTSUP, "T > 32 frames not supported");
-  if (is_bf16(h)) {
-    if (h->cfg.pos_emb_h * h->cfg.pos_emb_w != 256)
-      return fail(VP_ENOTSUP, "bf16 spatial attention kernel needs a 16x16 patch grid");
-    if (T > 16) return fail(VP_ENOTSUP, "bf16 temporal attention kernel needs T <= 16");
-  }
+  if (B * T * (H / P) * (W / P) > 0x7f000000) return fail(VP_ENOTSUP, "too many tokens");
   return VP_OK;
 }
 
@@ -467,9 +470,14 @@ struct Fwd {
           if (bf) return attention_long_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, s);
           return attention_masked(big, hb, 0, num_seq, S, NH, cap, nullptr, 0, s);
         }
-        if (!bf) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, cap, pad, s);
+        // other patch grids (S != 256) and T > 16 use the generic fp32-math kernel
+        if (!bf) {
+          if (S <= 256) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, cap, pad, s);
+          return attention_masked(big, hb, 0, num_seq, S, NH, cap, pad, 0, s);
+        }
         if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, cap, pad, s);
-        return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s); }));
+        if (S <= 16) return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s);
+        return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s); }));
       VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {
         return gemm(fold ? EPI_RESID_BF16_ST : epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1,
                     nullptr); }));

@@ -91,8 +91,9 @@ hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int hea
 
 // ---- elementwise / normalisation (elementwise.hip) ----
 enum RowPerm { PERM_NONE = 0, PERM_BTN_TO_BNT = 1, PERM_BNT_TO_BTN = 2 };
-// video [BT, H, W, C] (f32 or bf16) -> patches [BT*np, kpad] (bf16 or f32), zero-padded K.
-hipError_t patchify(const void* video, int in_is_bf16, void* patches, int out_is_bf16, int BT,
+// video [BT, H, W, C] (in_dtype 0 f32, 1 bf16, 2 uint8 normalised /255) -> patches [BT*np, kpad]
+// (bf16 or f32), zero-padded K.
+hipError_t patchify(const void* video, int in_dtype, void* patches, int out_is_bf16, int BT,
                     int H, int W, int C, int P, int kpad, hipStream_t s);
 // LayerNorm over D of fp32 or bf16 rows; gamma already holds (1 + scale).  Output row r goes
 // to row perm(r); `add` (optional, fp32 [add_rows][D]) is added by the *output* row's t index.

@@ -15,7 +15,7 @@ _LIB_NAME = "libvideoprism_hip.so"
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
 
 VP_OK, VP_EINVAL, VP_ENOMEM, VP_EHIP, VP_ESTATE, VP_ENOTSUP = range(6)
-VP_F32, VP_BF16 = 0, 1
+VP_F32, VP_BF16, VP_U8 = 0, 1, 2
 
 EPI_STORE, EPI_GELU, EPI_RESID, EPI_POS, EPI_RESID_FFN = 0, 1, 2, 3, 4
 # bf16 residual stream variants (bf16 resid / out; bf16 precision only)
@@ -69,6 +69,7 @@ _SIGNATURES = {
     "vp_param_count": (c_int, [c_void_p, POINTER(c_int)]),
     "vp_param_name": (c_int, [c_void_p, c_int, POINTER(c_char_p)]),
     "vp_finalize": (c_int, [c_void_p]),
+    "vp_prepare_geometry": (c_int, [c_void_p, c_int64, c_int64]),
     "vp_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "vp_forward": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -182,6 +183,8 @@ def _prec(t):
         return VP_BF16
     if t.dtype == torch.float32:
         return VP_F32
+    if t.dtype == torch.uint8:
+        return VP_U8
     raise TypeError(f"unsupported dtype {t.dtype}")
 
 

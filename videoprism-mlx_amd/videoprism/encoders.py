@@ -89,6 +89,7 @@ class Engine:
             self._h = None
             raise
         self._ws = None
+        self._grids = set()
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -123,9 +124,9 @@ class Engine:
         if C != 3:
             raise ValueError("inputs must have 3 channels")
         video = video.contiguous()
-        in_dt = _native.VP_BF16 if video.dtype == torch.bfloat16 else _native.VP_F32
-        if video.dtype not in (torch.bfloat16, torch.float32):
+        if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
             video = video.float()
+        in_dt = _native._prec(video)  # uint8 frames are normalised /255 on device
         out_dtype = out_dtype or (torch.bfloat16 if self.bf16 else torch.float32)
         P = self.cfg["patch_size"]
         if H % P or W % P:
@@ -133,6 +134,9 @@ class Engine:
                              f"of patch_size ({P}).")
         N = (H // P) * (W // P)
         D = self.cfg["model_dim"]
+        if (H, W) not in self._grids:  # interpolated spatial pos-emb for this frame size
+            _native.call("vp_prepare_geometry", self._h, H, W)
+            self._grids.add((H, W))
         if out is None:
             out = torch.empty((B, T * N, D), dtype=out_dtype, device=video.device)
         sp = torch.empty_like(out) if want_spatial else None
@@ -217,7 +221,11 @@ class FactorizedEncoder:
         torch = _torch()
         as_numpy = not isinstance(inputs, torch.Tensor)
         if as_numpy:
-            x = torch.from_numpy(np.ascontiguousarray(np.asarray(inputs, dtype=np.float32)))
+            arr = np.asarray(inputs)
+            # uint8 frames travel as bytes (4x less H2D than fp32) and are normalised /255 on
+            # device exactly as video_utils.py:94
+            x = torch.from_numpy(np.ascontiguousarray(arr if arr.dtype == np.uint8 else
+                                                      arr.astype(np.float32, copy=False)))
             device = torch.cuda.current_device()
             x = x.to(f"cuda:{device}")
         else:
@@ -284,6 +292,7 @@ class ClipEngine:
             self._h = None
             raise
         self._ws = {}
+        self._grids = set()
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -323,11 +332,14 @@ class ClipEngine:
             raise ValueError(f"Image height ({H}) and width ({W}) should be multiples "
                              f"of patch_size ({P}).")
         video = video.contiguous()
-        if video.dtype not in (torch.bfloat16, torch.float32):
+        if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
             video = video.float()
-        in_dt = _native.VP_BF16 if video.dtype == torch.bfloat16 else _native.VP_F32
+        in_dt = _native._prec(video)  # uint8 frames are normalised /255 on device
         D = self.cfg["model_dim"]
         N = (H // P) * (W // P)
+        if (H, W) not in self._grids:
+            _native.call("vp_prepare_geometry", self.video_handle(), H, W)
+            self._grids.add((H, W))
         fdt = torch.bfloat16 if self.bf16 else torch.float32
         dev = video.device
         vemb = torch.empty((B, D), dtype=torch.float32, device=dev)
@@ -453,8 +465,12 @@ class FactorizedVideoCLIP:
         video_emb = text_emb = None
         outputs = {}
         if inputs is not None:
-            x = inputs if isinstance(inputs, torch.Tensor) else torch.from_numpy(
-                np.ascontiguousarray(np.asarray(inputs, dtype=np.float32)))
+            if isinstance(inputs, torch.Tensor):
+                x = inputs
+            else:
+                arr = np.asarray(inputs)
+                x = torch.from_numpy(np.ascontiguousarray(
+                    arr if arr.dtype == np.uint8 else arr.astype(np.float32, copy=False)))
             x = x.to(dev)
             if x.dim() != 5:
                 raise ValueError(f"inputs must be [B, T, H, W, 3], got {tuple(x.shape)}")
