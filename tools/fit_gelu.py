@@ -50,3 +50,21 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def fit_tanh(y0=0.48, deg=3):
+    """Capped-softmax numerator exp(cap*tanh(x/cap)) = exp2(log2e * x * T((x/cap)^2)) for
+    |x| <= y0*cap, T(v) = tanh(sqrt v)/sqrt v fitted on v in [0, y0^2] (relative error)."""
+    v = np.linspace(1e-12, y0 * y0, 20001)
+    T = np.tanh(np.sqrt(v)) / np.sqrt(v)
+    c = fit(deg, v, T)
+    err = np.abs((horner32(c, v) - T) / T).max()
+    return c, err
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "tanh":
+    for y0 in (0.4, 0.48, 0.6):
+        for deg in (2, 3, 4):
+            c, err = fit_tanh(y0, deg)
+            print(f"tanh y0={y0} deg={deg}: rel err {err:.2e} (x*err*log2e at x=y0*50: {err*y0*50*1.4427:.2e})",
+                  ", ".join(f"{float(np.float32(a))!r}" for a in c))
