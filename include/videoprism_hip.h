@@ -115,6 +115,10 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
 int vp_profile_enable(vp_handle* h, int capacity);
 int vp_profile_read(vp_handle* h, int nclass, double* ms, double* flops, double* bytes,
                     int64_t* launches);
+/* Only launches of the classes whose bit is set in class_mask get events (default: all).  Each
+ * event pair costs the stream a little, so bench.py times the dominant class alone in its timed
+ * region and takes the per-class breakdown from a separate profiled step. */
+int vp_profile_set_mask(vp_handle* h, uint32_t class_mask);
 int vp_profile_class_count(void);
 int vp_profile_class_name(int cls, const char** name);
 

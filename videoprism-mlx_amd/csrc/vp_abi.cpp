@@ -328,6 +328,12 @@ int vp_profile_enable(vp_handle* h, int capacity) {
   return VP_OK;
 }
 
+int vp_profile_set_mask(vp_handle* h, uint32_t class_mask) {
+  if (!h) return fail(VP_EINVAL, "null handle");
+  h->prof.mask = class_mask;
+  return VP_OK;
+}
+
 int vp_profile_read(vp_handle* h, int nclass, double* ms, double* flops, double* bytes,
                     int64_t* launches) {
   if (!h || nclass < PC_COUNT || !ms || !flops || !bytes || !launches)

@@ -106,6 +106,7 @@ inline const char* kProfNames[PC_COUNT] = {"patchify", "gemm_patch_embed", "laye
 // HIP-event profiler: start/stop events around each launch on the launch stream.
 struct Profiler {
   int cap = 0, used = 0;
+  uint32_t mask = 0xffffffffu;  // kernel classes that get events (vp_profile_set_mask)
   std::vector<hipEvent_t> ev;
   std::vector<int> cls;
   std::vector<double> flops, bytes;
@@ -408,7 +409,7 @@ struct Fwd {
   // profiled launch: records events around `fn` when vp_profile_enable() is active
   template <class Fn>
   hipError_t rec(int cls, double flops, double bytes, Fn&& fn) {
-    if (!pf || pf->used >= pf->cap) return fn();
+    if (!pf || pf->used >= pf->cap || !((pf->mask >> cls) & 1u)) return fn();
     const int i = pf->used++;
     hipError_t e = hipEventRecord(pf->ev[2 * i], s);
     if (e != hipSuccess) return e;

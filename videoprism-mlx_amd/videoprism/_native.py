@@ -76,6 +76,7 @@ _SIGNATURES = {
     "vp_profile_enable": (c_int, [c_void_p, c_int]),
     "vp_profile_read": (c_int, [c_void_p, c_int, POINTER(ctypes.c_double), POINTER(ctypes.c_double),
                                 POINTER(ctypes.c_double), POINTER(c_int64)]),
+    "vp_profile_set_mask": (c_int, [c_void_p, ctypes.c_uint32]),
     "vp_profile_class_count": (c_int, []),
     "vp_profile_class_name": (c_int, [c_int, POINTER(c_char_p)]),
     "vp_op_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64,

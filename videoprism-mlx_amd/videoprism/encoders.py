@@ -41,6 +41,20 @@ def _profile_enable(handle, capacity: int) -> None:
     _native.call("vp_profile_enable", handle, int(capacity))
 
 
+def _profile_set_mask(handle, names=None) -> None:
+    """Restrict events to the named kernel classes (None: all)."""
+    mask = 0xFFFFFFFF
+    if names is not None:
+        lib = _native.load()
+        mask = 0
+        for i in range(lib.vp_profile_class_count()):
+            name = ctypes.c_char_p()
+            _native.call("vp_profile_class_name", i, ctypes.byref(name))
+            if name.value.decode() in names:
+                mask |= 1 << i
+    _native.call("vp_profile_set_mask", handle, mask)
+
+
 def _profile_read(handle) -> dict:
     """{kernel class: {ms, flops, bytes, launches}} since the previous read (vp_profile_read)."""
     lib = _native.load()
@@ -103,6 +117,9 @@ class Engine:
 
     def profile_read(self) -> dict:
         return _profile_read(self._h)
+
+    def profile_only(self, names=None) -> None:
+        _profile_set_mask(self._h, names)
 
     def workspace(self, B, T, H, W):
         torch = _torch()
@@ -311,6 +328,9 @@ class ClipEngine:
 
     def profile_read(self) -> dict:
         return _profile_read(self.video_handle())
+
+    def profile_only(self, names=None) -> None:
+        _profile_set_mask(self.video_handle(), names)
 
     def _workspace(self, key, nbytes):
         torch = _torch()
