@@ -66,39 +66,44 @@ __device__ __forceinline__ float to_f(TI v) {
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void patchify_band_kernel(const TI* __restrict__ video, TO* __restrict__ out,
                                                             int H, int W, int C, int P, int kpad) {
-  extern __shared__ float band[];
+  // the band is staged in the OUTPUT dtype: exact (the value is rounded once either way) and,
+  // for bf16, 31 KiB per workgroup so five workgroups share a CU
+  extern __shared__ __attribute__((aligned(16))) char band_raw[];
+  TO* band = reinterpret_cast<TO*>(band_raw);
   const int gm = H / P, gn = W / P;
   const int bt = blockIdx.x / gm, mi = blockIdx.x % gm;
   const int rowlen = W * C;
   const int n = P * rowlen;
   const TI* src = video + ((int64_t)bt * H + (int64_t)mi * P) * rowlen;
+  auto put = [&](int i, float v) {
+    if constexpr (sizeof(TO) == 2) band[i] = f2bf(v);
+    else band[i] = v;
+  };
   constexpr int V = 16 / sizeof(TI);  // elements per 16-byte load
   if (rowlen % V == 0) {  // every row start (and the band) 16-byte aligned
     typedef TI vec_t __attribute__((ext_vector_type(V)));
     for (int i = threadIdx.x; i < n / V; i += 256) {
       const vec_t x = *reinterpret_cast<const vec_t*>(src + (int64_t)i * V);
 #pragma unroll
-      for (int j = 0; j < V; ++j) band[i * V + j] = to_f<TI>(x[j]);
+      for (int j = 0; j < V; ++j) put(i * V + j, to_f<TI>(x[j]));
     }
   } else {
-    for (int i = threadIdx.x; i < n; i += 256) band[i] = to_f<TI>(src[i]);
+    for (int i = threadIdx.x; i < n; i += 256) put(i, to_f<TI>(src[i]));
   }
   __syncthreads();
   const int pc = P * C, kreal = P * pc, groups = kpad / 8;
   TO* dst = out + ((int64_t)bt * gm * gn + (int64_t)mi * gn) * kpad;
   for (int gi = threadIdx.x; gi < gn * groups; gi += 256) {
     const int ni = gi / groups, k0 = (gi % groups) * 8;
-    float v[8];
+    TO v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = k0 + j;
       const int p = k / pc;
-      v[j] = k < kreal ? band[p * rowlen + ni * pc + (k - p * pc)] : 0.0f;
+      v[j] = k < kreal ? band[p * rowlen + ni * pc + (k - p * pc)] : TO(0);
     }
     if constexpr (sizeof(TO) == 2) {
-      *reinterpret_cast<uint4*>(dst + (int64_t)ni * kpad + k0) =
-          make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                     pack_bf16x2(v[6], v[7]));
+      *reinterpret_cast<uint4*>(dst + (int64_t)ni * kpad + k0) = *reinterpret_cast<const uint4*>(v);
     } else {
       float4* op = reinterpret_cast<float4*>(dst + (int64_t)ni * kpad + k0);
       op[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -372,7 +377,7 @@ hipError_t patchify(const void* video, int in_dtype, void* patches, int out_is_b
   if (kpad % 8 || kpad < P * P * C || H % P || W % P || in_dtype < 0 || in_dtype > 2) return hipErrorInvalidValue;
   const int64_t work = (int64_t)BT * (H / P) * (W / P) * (kpad / 8);
   const int grid = grid_for(work, 256);
-  const size_t band_bytes = (size_t)P * W * C * 4;
+  const size_t band_bytes = (size_t)P * W * C * (out_is_bf16 ? 2 : 4);
   const bool aligned = ((uintptr_t)video & 15) == 0;
   auto go = [&](auto in_tag) {
     using TI = decltype(in_tag);
