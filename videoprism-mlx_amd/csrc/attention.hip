@@ -61,7 +61,7 @@ constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 template <bool MASK, int DIAG = 0, bool STAGE = false>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
-    const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec) {
+    const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec, CapPoly cp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + kSpS * 128;
@@ -161,9 +161,14 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     }
     // numerators: register i <-> key kt*32 + (i&3) + 8(i>>2) + 4*half
     float p[16];
+    // (the one-transcendental numerator of capped_exp16 is not used here: this kernel is bound by
+    // its q|k|v stream, and it moved the full-depth LvT-B bf16 embedding across the 1e-3 bar)
+    (void)cp;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = (DIAG & 1) ? x[i] : capped_exp(x[i], c1, c2);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float e = (DIAG & 1) ? x[i] : capped_exp(x[i], c1, c2);
+      float e = p[i];
       if constexpr (MASK) {
         const int key = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
         e = all_masked ? 1.0f : (kp[key] != 0.0f ? 0.0f : e);
@@ -450,10 +455,10 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   const int64_t D = heads * 64;
   if (key_pad)
     hipLaunchKernelGGL((attn_spatial_kernel<true, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
-                       key_pad, rev, 3 * D, (int64_t)64, D);
+                       key_pad, rev, 3 * D, (int64_t)64, D, make_cap_poly(cap));
   else
     hipLaunchKernelGGL((attn_spatial_kernel<false, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
-                       key_pad, rev, 3 * D, (int64_t)64, D);
+                       key_pad, rev, 3 * D, (int64_t)64, D, make_cap_poly(cap));
   return hipGetLastError();
 }
 
@@ -467,7 +472,8 @@ hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int nu
   auto go = [&](const void* fn, auto kern) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, nullptr, 0, rs, hs, sec);
+    hipLaunchKernelGGL(kern, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, nullptr, 0, rs, hs, sec,
+                       make_cap_poly(cap));
     return hipGetLastError();
   };
   if (diag >= 16) {

@@ -33,16 +33,6 @@ __device__ __forceinline__ float capped_exp(float x, float two_log2e_over_cap, f
   return __builtin_amdgcn_exp2f(cap_log2e - 2.0f * cap_log2e * r);
 }
 
-// The same numerator with ONE transcendental where every logit of the wave's tile has
-// |x| <= 0.48 cap: cap*tanh(x/cap) = x*T((x/cap)^2), T(v) = tanh(sqrt v)/sqrt v fitted on
-// v in [0, 0.48^2] by a cubic (relative error 4.5e-7, tools/fit_gelu.py fit_tanh), so
-// exp(cap*tanh(x/cap)) = exp2(x * P(x^2)) with P's coefficients k_i = log2e t_i / cap^(2i)
-// folded on the host; tiles holding a larger logit take the exact three-transcendental path
-// (wave-uniform branch).  5 VALU + 1 transcendental instead of 3 + 3 per logit.
-struct CapPoly {
-  float k0, k1, k2, k3, x0;
-};
-
 __device__ __forceinline__ int swzK(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swzV(int row) { return ((row >> 1) & 1) << 2; }
 
@@ -149,20 +139,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
         x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       }
       float p[16];
-      float mx = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
-      if (__builtin_amdgcn_ballot_w64(mx > cp.x0) == 0) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float u = x[i] * x[i];
-          const float P = fmaf(fmaf(fmaf(cp.k3, u, cp.k2), u, cp.k1), u, cp.k0);
-          p[i] = __builtin_amdgcn_exp2f(x[i] * P);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) p[i] = capped_exp(x[i], c1, c2);
-      }
+      capped_exp16(x, p, c1, c2, cp);
 #pragma unroll
       for (int i = 0; i < 16; ++i) lsum += p[i];
       bf16x8 pf[2];
@@ -332,11 +309,7 @@ hipError_t attention_long_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S,
   const int64_t grid = (int64_t)num_seq * heads * nqb;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const int xcd_map = grid % 8 == 0 ? 1 : 0;
-  // cubic T(v) ~ tanh(sqrt v)/sqrt v on v in [0, 0.48^2] (tools/fit_gelu.py fit_tanh(0.48, 3))
-  const double t[4] = {0.9999995827674866, -0.33327752351760864, 0.1321016252040863, -0.045063190162181854};
-  const double l2e = 1.4426950408889634, c2 = (double)cap * cap;
-  CapPoly cp{(float)(l2e * t[0]), (float)(l2e * t[1] / c2), (float)(l2e * t[2] / (c2 * c2)),
-             (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap};
+  const CapPoly cp = make_cap_poly(cap);
   hipLaunchKernelGGL(attn_long_kernel, dim3((unsigned)grid), dim3(kLgThreads), kLgLds, s, qkv, o, S, heads,
                      nqb, cap, xcd_map, cp);
   return hipGetLastError();

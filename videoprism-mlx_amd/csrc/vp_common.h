@@ -56,6 +56,47 @@ __device__ __forceinline__ int wave_id() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 }
 
+// ---- capped-softmax numerators exp(cap * tanh(x / cap)) (layers.py:586-594, :650-654) ----
+// exact form: tanh(y) = 1 - 2 / (exp(2y) + 1), three transcendentals, saturates correctly
+__device__ __forceinline__ float capped_exp_exact(float x, float two_log2e_over_cap, float cap_log2e) {
+  const float t = __builtin_amdgcn_exp2f(x * two_log2e_over_cap);
+  const float r = __builtin_amdgcn_rcpf(t + 1.0f);
+  return __builtin_amdgcn_exp2f(cap_log2e - 2.0f * cap_log2e * r);
+}
+
+// One transcendental where every logit of the wave's 32x32 tile has |x| <= 0.48 cap:
+// cap*tanh(x/cap) = x*T((x/cap)^2), T(v) = tanh(sqrt v)/sqrt v fitted on v in [0, 0.48^2] by a
+// cubic (relative error 4.5e-7, tools/fit_gelu.py fit_tanh), so the numerator is
+// exp2(x * P(x^2)) with k_i = log2e t_i / cap^(2i) folded on the host (make_cap_poly); tiles
+// holding a larger logit take the exact path (wave-uniform branch).
+struct CapPoly {
+  float k0, k1, k2, k3, x0;
+};
+
+inline CapPoly make_cap_poly(float cap) {
+  const double t[4] = {0.9999995827674866, -0.33327752351760864, 0.1321016252040863, -0.045063190162181854};
+  const double l2e = 1.4426950408889634, c2 = (double)cap * cap;
+  return CapPoly{(float)(l2e * t[0]), (float)(l2e * t[1] / c2), (float)(l2e * t[2] / (c2 * c2)),
+                 (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap};
+}
+
+__device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
+  float mx = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
+  if (__builtin_amdgcn_ballot_w64(mx > cp.x0) == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float u = x[i] * x[i];
+      const float P = fmaf(fmaf(fmaf(cp.k3, u, cp.k2), u, cp.k1), u, cp.k0);
+      p[i] = __builtin_amdgcn_exp2f(x[i] * P);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = capped_exp_exact(x[i], c1, c2);
+  }
+}
+
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 }  // namespace vp
