@@ -161,11 +161,14 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     }
     // numerators: register i <-> key kt*32 + (i&3) + 8(i>>2) + 4*half
     float p[16];
-    // (the one-transcendental numerator of capped_exp16 is not used here: this kernel is bound by
-    // its q|k|v stream, and it moved the full-depth LvT-B bf16 embedding across the 1e-3 bar)
-    (void)cp;
+    // DIAG 4: the one-transcendental numerator of capped_exp16 (A/B build; production keeps the
+    // exact form -- the polynomial moved the full-depth LvT-B bf16 embedding across the 1e-3 bar)
+    if constexpr ((DIAG & 4) != 0) {
+      capped_exp16(x, p, c1, c2, cp);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = (DIAG & 1) ? x[i] : capped_exp(x[i], c1, c2);
+      for (int i = 0; i < 16; ++i) p[i] = (DIAG & 1) ? x[i] : capped_exp(x[i], c1, c2);
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float e = p[i];
@@ -476,6 +479,8 @@ hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int nu
                        make_cap_poly(cap));
     return hipGetLastError();
   };
+  if (diag == 4 + 32)  // staged stores + polynomial numerator
+    return go((const void*)attn_spatial_kernel<false, 4, true>, attn_spatial_kernel<false, 4, true>);
   if (diag >= 16) {
     if (diag & 32) return go((const void*)attn_spatial_kernel<false, 0, true>, attn_spatial_kernel<false, 0, true>);
     return go((const void*)attn_spatial_kernel<false, 0, false>, attn_spatial_kernel<false, 0, false>);
