@@ -223,6 +223,31 @@ int vp_clip_encode_text(vp_clip* c, const int32_t* ids, const float* paddings, i
                         int64_t L, int normalize, float* text_emb, void* workspace,
                         size_t ws_bytes, void* stream);
 
+/* ---------------- video classifier: FactorizedVideoClassifier (encoders.py:583-653) ----------------
+ * Replaces encoders.FactorizedVideoClassifier(encoder_params, num_classes).apply(...) and the
+ * models.videoprism_vc_v1_{base,large}(num_classes) builders (models.py:195-216).  Leaves:
+ * 'encoder/...' (the FactorizedEncoder leaves), 'atten_pooler/...' (AttenTokenPoolingLayer with
+ * hidden D, 12 leaves), 'projection/linear/{kernel [D, C], bias [C]}': 54 in all
+ * (encoders_test.py:224).
+ *   logits      device [B, num_classes] fp32
+ *   embeddings  device [B, D] fp32 'global_embeddings' (the pooled vector) or NULL
+ *   spatial_out / spatiotemporal_out as vp_clip_encode_video */
+typedef struct vp_classifier vp_classifier;
+int vp_classifier_create(const vp_config* cfg, int num_classes, int device, vp_classifier** out);
+int vp_classifier_destroy(vp_classifier* c);
+int vp_classifier_set_param(vp_classifier* c, const char* name, const float* host_data,
+                            const int64_t* shape, int ndim);
+int vp_classifier_param_count(const vp_classifier* c, int* count);
+int vp_classifier_param_name(const vp_classifier* c, int index, const char** name);
+int vp_classifier_finalize(vp_classifier* c);
+int vp_classifier_video_handle(vp_classifier* c, vp_handle** video);
+int vp_classifier_workspace_bytes(const vp_classifier* c, int64_t B, int64_t T, int64_t H, int64_t W,
+                                  size_t* bytes);
+int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int64_t B, int64_t T,
+                          int64_t H, int64_t W, const float* frame_paddings, float* logits,
+                          float* embeddings, void* spatial_out, void* spatiotemporal_out,
+                          int out_dtype, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -551,3 +551,22 @@ def masked_attention(q, k, v, cap: float, key_pad=None, causal: bool = False):
     pad = np.zeros(q.shape[:2]) if key_pad is None else np.asarray(key_pad, np.float64)
     mask = attention_masks_for_fprop(pad, causal)[:, 0]
     return np.matmul(softmax(apply_mask_to_logits(logits, mask)), v)
+
+
+def video_classifier(params, cfg: dict, inputs, mode: str = "f64", return_intermediate=False,
+                     frame_paddings=None):
+    """encoders.py:583-653 FactorizedVideoClassifier.__call__ -> (logits [B, C], outputs).
+    cfg: the encoder_params (a FactorizedEncoder CONFIGS entry).  The pooler is
+    AttenTokenPoolingLayer(num_heads, hidden_dim=model_dim, num_queries=1) with its defaults
+    (per-dim scale, LayerNorm), applied with paddings None."""
+    nm = Numerics(mode)
+    feats, outputs = factorized_encoder(params["encoder"], inputs, cfg, mode, frame_paddings,
+                                        return_intermediate)
+    if _contains(return_intermediate, "spatiotemporal_features"):
+        outputs["spatiotemporal_features"] = feats
+    emb = atten_token_pooling(feats, params["atten_pooler"], nm, cfg["num_heads"],
+                              cfg["model_dim"])[:, 0]
+    if _contains(return_intermediate, "global_embeddings"):
+        outputs["global_embeddings"] = emb
+    proj = params["projection"]["linear"]
+    return dense(emb, proj["kernel"], proj["bias"], nm), outputs

@@ -131,3 +131,43 @@ def test_host_clip_api_surface():
         models_mlx.load_model("videoprism_lvt_public_v1_base", weights_path="/nonexistent.npz")
     with pytest.raises(ValueError, match="not found"):
         models_mlx.load_model("videoprism_lvt_public_v1_giant")
+
+
+# ---------------- FactorizedVideoClassifier (encoders.py:583-653) ----------------
+ENC_TINY = dict(patch_size=4, pos_emb_shape=(16, 16, 16), model_dim=8, num_spatial_layers=2,
+                num_temporal_layers=2, num_heads=2, mlp_dim=4, atten_logit_cap=50.0)
+
+
+def test_classifier_leaf_count():
+    """encoders_test.py:224 — 54 leaves."""
+    assert len(params.classifier_leaf_specs(ENC_TINY, 10)) == 54
+
+
+@pytest.mark.parametrize("ri", [False, True])
+def test_classifier_tiny_shapes(ri):
+    """encoders_test.py:205-240: logits (B, 10); intermediates spatial / spatiotemporal / global."""
+    var = params.synthetic_params(ENC_TINY, 0, specs=params.classifier_leaf_specs(ENC_TINY, 10))
+    x = np.random.default_rng(0).normal(0, 0.1, (2, 4, 16, 16, 3)).astype(np.float32)
+    logits, out = orc.video_classifier(var["params"], ENC_TINY, x, return_intermediate=ri)
+    assert logits.shape == (2, 10)
+    if ri:
+        assert set(out) == {"spatial_features", "spatiotemporal_features", "global_embeddings"}
+        assert out["global_embeddings"].shape == (2, 8)
+    else:
+        assert out == {}
+
+
+def test_classifier_registry_and_loader():
+    m = models.videoprism_vc_v1_large(7)
+    assert isinstance(m, encoders.FactorizedVideoClassifier)
+    assert m.num_classes == 7 and m.encoder_params["model_dim"] == 1024
+    mm, var = models_mlx.load_classifier("videoprism_lvt_public_v1_base", 3)
+    assert len(params.flatten(var["params"])) == 54
+    assert var["params"]["projection"]["linear"]["kernel"].shape == (768, 3)
+
+
+def test_oracle_classifier_vs_torch_restatement():
+    var = params.synthetic_params(ENC_TINY, 3, specs=params.classifier_leaf_specs(ENC_TINY, 10))
+    x = np.random.default_rng(3).normal(0, 0.1, (2, 4, 16, 16, 3)).astype(np.float32)
+    logits, _ = orc.video_classifier(var["params"], ENC_TINY, x)
+    np.testing.assert_allclose(logits, torch_restatement.video_classifier(var["params"], ENC_TINY, x), atol=1e-11)

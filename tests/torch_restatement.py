@@ -170,12 +170,13 @@ def _gelu(a):
     return 0.5 * a * (1.0 + torch.erf(a / 2 ** 0.5))
 
 
-def pooler(tokens, p, heads):
-    """AttenTokenPoolingLayer: one learned query, dh = 4D/heads, per-dim scale, no cap, LN."""
+def pooler(tokens, p, heads, hidden=None):
+    """AttenTokenPoolingLayer: one learned query, dh = hidden/heads (4D for the CLIP pooler, D for
+    the classifier's), per-dim scale, no cap, LN."""
     x = _t(tokens)
     D = x.shape[-1]
     pa = p["pooling_attention"]
-    dh = 4 * D // heads
+    dh = (hidden or 4 * D) // heads
     q = torch.einsum("d,dnh->nh", _t(p["pooling_attention_query"])[0], _t(pa["query"]["w"]))
     q = (q + _t(pa["query"]["b"])) * (1.442695041 / dh ** 0.5) * F.softplus(_t(pa["per_dim_scale"]["per_dim_scale"]))
     k = torch.einsum("bsd,dnh->bsnh", x, _t(pa["key"]["w"])) + _t(pa["key"]["b"])
@@ -218,3 +219,11 @@ def video_clip(params, cfg, video, ids, paddings, frame_paddings=None):
                        cfg["enable_causal_atten"], torch.relu)
     temb = _l2n(_ln(y, te["unimodal_ln"])[:, -1])
     return vemb.numpy(), temb.numpy(), femb.numpy()
+
+
+def video_classifier(params, cfg, video):
+    """encoders.py:583-653 -> logits (fp64 numpy)."""
+    feats, _ = factorized_encoder(params["encoder"], video, cfg)
+    emb = pooler(_t(feats), params["atten_pooler"], cfg["num_heads"], hidden=cfg["model_dim"])
+    proj = params["projection"]["linear"]
+    return (emb @ _t(proj["kernel"]) + _t(proj["bias"])).numpy()

@@ -14,6 +14,16 @@ namespace {
 constexpr int kMaxTextLen = 1024;  // L + 1 (CLS) tokens; TEXT_MAX_LEN is 64 (models.py:53)
 }
 
+// AttenTokenPoolingLayer weights, packed (see pack_pooler): U [H][D] (query folded into the key
+// projection), Ut = bf16 hi|lo halves of U for the MFMA logits, Wv^T [H][D][dp], bv [H][dp],
+// Wpost^T [H*dp][D], bpost [D], LayerNorm gamma (1 + scale) / beta
+struct PoolerW {
+  void* Ut = nullptr;
+  float *U = nullptr, *WvT = nullptr, *bv = nullptr, *WpT = nullptr, *bp = nullptr;
+  float *ln_g = nullptr, *ln_b = nullptr;
+  int dp = 0;
+};
+
 struct vp_clip {
   vp_clip_config cfg;
   int device = 0;
@@ -25,10 +35,7 @@ struct vp_clip {
   std::vector<vpi::DevBuf> allocs;
   bool bf16() const { return cfg.video.fprop_dtype == VP_BF16; }
   std::vector<vpi::LayerW> aux, text;
-  // contrastive pooler (fp32): U [H][D], Wv^T [H][D][dp], bv [H][dp], Wpost^T [H*dp][D], bpost [D]
-  void* pUt = nullptr;  // [32][D] bf16: U_hi rows 0..H-1, U_lo rows H..2H-1, zeros
-  float *pU = nullptr, *pWvT = nullptr, *pbv = nullptr, *pWpT = nullptr, *pbp = nullptr;
-  float *pln_g = nullptr, *pln_b = nullptr;
+  PoolerW pool;  // contrastive_vision_pooler (hidden 4D)
   // text tower: token table [V][D] (fprop dtype), cls [D], sinusoidal table [kMaxTextLen][D]
   void* tok = nullptr;
   float *cls = nullptr, *tpos = nullptr, *uln_g = nullptr, *uln_b = nullptr;
@@ -40,11 +47,12 @@ struct ClipVideoWs {
   size_t inner = 0, feat = 0, logits = 0, stats = 0, zpart = 0, z = 0, enc = 0, pooled = 0, total = 0;
 };
 
-ClipVideoWs clip_video_ws(const vp_clip* c, int64_t B, int64_t T, int64_t H, int64_t W, size_t inner_bytes) {
-  const vp_config& v = c->cfg.video;
+// vision features + pooler scratch for G <= B*T groups; dp = the pooler's dim_per_head
+ClipVideoWs pool_video_ws(const vp_config& v, int64_t B, int64_t T, int64_t H, int64_t W, size_t inner_bytes,
+                          int64_t dp) {
   const int64_t P = v.patch_size, N = (H / P) * (W / P), M = B * T * N;
-  const int64_t D = v.model_dim, NH = v.num_heads, dp = 4 * D / NH;
-  const size_t es = c->bf16() ? 2 : 4;
+  const int64_t D = v.model_dim, NH = v.num_heads;
+  const size_t es = v.fprop_dtype == VP_BF16 ? 2 : 4;
   const int64_t gc = std::max<int64_t>(B * vp::pool_chunks((int)(T * N)), B * T * vp::pool_chunks((int)N));
   ClipVideoWs L;
   size_t off = 0;
@@ -58,6 +66,10 @@ ClipVideoWs clip_video_ws(const vp_clip* c, int64_t B, int64_t T, int64_t H, int
   L.pooled = off; off = align256(off + (size_t)B * T * D * 4);
   L.total = off;
   return L;
+}
+
+ClipVideoWs clip_video_ws(const vp_clip* c, int64_t B, int64_t T, int64_t H, int64_t W, size_t inner_bytes) {
+  return pool_video_ws(c->cfg.video, B, T, H, W, inner_bytes, 4 * c->cfg.video.model_dim / c->cfg.video.num_heads);
 }
 
 struct ClipTextWs {
@@ -79,13 +91,9 @@ ClipTextWs clip_text_ws(const vp_clip* c, int64_t Q, int64_t L) {
   return w;
 }
 
-void build_clip_expected(vp_clip* c) {
-  const vp_clip_config& cc = c->cfg;
-  const int64_t D = cc.video.model_dim, NH = cc.video.num_heads, dp = 4 * D / NH;
-  if (cc.num_auxiliary_layers > 0)
-    add_stack_expected(c, "auxiliary_encoder/transformers_stack/x_layers/", cc.num_auxiliary_layers, D,
-                       cc.video.mlp_dim, NH);
-  const std::string pre = "contrastive_vision_pooler/";
+// the 12 leaves of an AttenTokenPoolingLayer (layers.py:1044-1136, layers_test.py:283)
+template <class Hd>
+void add_pooler_expected(Hd* c, const std::string& pre, int64_t D, int64_t NH, int64_t dp) {
   add_expected(c, pre + "pooling_attention_query", {1, D});
   add_expected(c, pre + "pooling_attention/per_dim_scale/per_dim_scale", {dp});
   for (const char* q : {"query", "key", "value"}) {
@@ -96,6 +104,15 @@ void build_clip_expected(vp_clip* c) {
   add_expected(c, pre + "pooling_attention/post/b", {D});
   add_expected(c, pre + "pooling_attention_layer_norm/scale", {D});
   add_expected(c, pre + "pooling_attention_layer_norm/bias", {D});
+}
+
+void build_clip_expected(vp_clip* c) {
+  const vp_clip_config& cc = c->cfg;
+  const int64_t D = cc.video.model_dim, NH = cc.video.num_heads, dp = 4 * D / NH;
+  if (cc.num_auxiliary_layers > 0)
+    add_stack_expected(c, "auxiliary_encoder/transformers_stack/x_layers/", cc.num_auxiliary_layers, D,
+                       cc.video.mlp_dim, NH);
+  add_pooler_expected(c, "contrastive_vision_pooler/", D, NH, dp);
   add_expected(c, "text_encoder/token_emb/emb_var", {(int64_t)cc.vocabulary_size, D});
   add_expected(c, "text_encoder/cls_emb", {1, 1, D});
   add_stack_expected(c, "text_encoder/unimodal_transformer/x_layers/", cc.num_unimodal_layers, D, 4 * D, NH);
@@ -105,10 +122,11 @@ void build_clip_expected(vp_clip* c) {
 
 // AttenTokenPoolingLayer (layers.py:1044-1136) with the query folded into the key projection
 // (see clip_kernels.hip): host packing in fp64.
-int pack_pooler(vp_clip* c) {
-  const int64_t D = c->cfg.video.model_dim, H = c->cfg.video.num_heads, dp = 4 * D / H;
-  const std::string pre = "contrastive_vision_pooler/pooling_attention/";
-  const auto& query = param_data(c, "contrastive_vision_pooler/pooling_attention_query");
+template <class Hd>
+int pack_pooler(Hd* c, const std::string& root, int64_t D, int64_t H, int64_t dp, PoolerW& pw) {
+  const std::string pre = root + "pooling_attention/";
+  pw.dp = (int)dp;
+  const auto& query = param_data(c, root + "pooling_attention_query");
   const auto& wq = param_data(c, pre + "query/w");
   const auto& bq = param_data(c, pre + "query/b");
   const auto& wk = param_data(c, pre + "key/w");
@@ -139,7 +157,7 @@ int pack_pooler(vp_clip* c) {
   for (int64_t n = 0; n < D; ++n)
     for (int64_t k = 0; k < H * dp; ++k) wpt[(size_t)k * D + n] = wp[(size_t)n * H * dp + k];
   std::vector<float> g(D);
-  const auto& sc = param_data(c, "contrastive_vision_pooler/pooling_attention_layer_norm/scale");
+  const auto& sc = param_data(c, root + "pooling_attention_layer_norm/scale");
   for (int64_t d = 0; d < D; ++d) g[d] = sc[d] + 1.0f;
   // bf16 hi/lo split of U for the MFMA logits kernel
   std::vector<uint16_t> ut((size_t)32 * D, 0);
@@ -154,12 +172,33 @@ int pack_pooler(vp_clip* c) {
       ut[(size_t)(H + h) * D + d] = host_f2bf(u - hf);
     }
   int rc;
-  if ((rc = dev_alloc(c, ut.size() * 2, &c->pUt))) return rc;
-  VP_HIP(hipMemcpy(c->pUt, ut.data(), ut.size() * 2, hipMemcpyHostToDevice));
-  if ((rc = upload_f32(c, U, &c->pU)) || (rc = upload_f32(c, wvt, &c->pWvT)) || (rc = upload_f32(c, bv, &c->pbv)) ||
-      (rc = upload_f32(c, wpt, &c->pWpT)) || (rc = upload_f32(c, bp, &c->pbp)) || (rc = upload_f32(c, g, &c->pln_g)) ||
-      (rc = upload_f32(c, param_data(c, "contrastive_vision_pooler/pooling_attention_layer_norm/bias"), &c->pln_b)))
+  if ((rc = dev_alloc(c, ut.size() * 2, &pw.Ut))) return rc;
+  VP_HIP(hipMemcpy(pw.Ut, ut.data(), ut.size() * 2, hipMemcpyHostToDevice));
+  if ((rc = upload_f32(c, U, &pw.U)) || (rc = upload_f32(c, wvt, &pw.WvT)) || (rc = upload_f32(c, bv, &pw.bv)) ||
+      (rc = upload_f32(c, wpt, &pw.WpT)) || (rc = upload_f32(c, bp, &pw.bp)) || (rc = upload_f32(c, g, &pw.ln_g)) ||
+      (rc = upload_f32(c, param_data(c, root + "pooling_attention_layer_norm/bias"), &pw.ln_b)))
     return rc;
+  return VP_OK;
+}
+
+// pooler over G groups of Sg rows of feat [G*Sg][D] -> dst [G][D] fp32 (LayerNorm, then L2 if do_l2)
+struct PoolScratch {
+  float *logits, *stats, *zpart, *z, *enc, *pooled;
+};
+
+int run_pooler(Fwd& f, const PoolerW& pw, const void* feat, int M, int G, int Sg, int D, int NH,
+               const PoolScratch& sc, int do_l2, float* dst) {
+  using namespace vp;
+  const int dp = pw.dp;
+  const double bytes = 2.0 * M * D * (f.bf ? 2 : 4);  // two streaming passes over the tokens
+  VP_HIP(f.rec(PC_POOL, 2.0 * 2.0 * M * D * NH, bytes, [&] {
+    hipError_t e = pool_logits(feat, f.bf, M, Sg, D, pw.U, (const bf16_t*)pw.Ut, NH, sc.logits, f.s);
+    if (e != hipSuccess) return e;
+    return pool_softmax_wsum(feat, f.bf, G, Sg, D, NH, sc.logits, sc.stats, sc.zpart, sc.z, f.s); }));
+  VP_HIP(small_gemm(sc.z, (int64_t)NH * D, D, pw.WvT, (int64_t)D * dp, pw.bv, dp, sc.enc, (int64_t)NH * dp, dp, G,
+                    dp, D, NH, f.s));
+  VP_HIP(small_gemm(sc.enc, (int64_t)NH * dp, 0, pw.WpT, 0, pw.bp, 0, sc.pooled, D, 0, G, D, NH * dp, 1, f.s));
+  VP_HIP(ln_l2_rows(sc.pooled, 0, D, G, D, pw.ln_g, pw.ln_b, do_l2, dst, f.s));
   return VP_OK;
 }
 
@@ -280,7 +319,10 @@ int vp_clip_finalize(vp_clip* c) {
       (rc = pack_stack(c, "auxiliary_encoder/transformers_stack/x_layers/", c->cfg.num_auxiliary_layers, v.model_dim,
                        v.mlp_dim, v.num_heads, c->bf16(), c->aux)))
     return rc;
-  if ((rc = pack_pooler(c)) || (rc = pack_text(c))) return rc;
+  if ((rc = pack_pooler(c, "contrastive_vision_pooler/", v.model_dim, v.num_heads, 4 * v.model_dim / v.num_heads,
+                        c->pool)) ||
+      (rc = pack_text(c)))
+    return rc;
   c->host.clear();
   c->finalized = true;
   return VP_OK;
@@ -318,7 +360,7 @@ int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B,
   const ClipVideoWs L = clip_video_ws(c, B, T, H, W, inner);
   if (ws_bytes < L.total) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(L.total));
   const vp_config& v = c->cfg.video;
-  const int P = v.patch_size, N = (int)((H / P) * (W / P)), D = v.model_dim, NH = v.num_heads, dp = 4 * D / NH;
+  const int P = v.patch_size, N = (int)((H / P) * (W / P)), D = v.model_dim, NH = v.num_heads;
   const int S = (int)T * N;
   const int64_t M64 = B * T * N;
   if (M64 > 0x7fffffff) return fail(VP_ENOTSUP, "too many tokens");
@@ -362,17 +404,9 @@ int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B,
   float* z = reinterpret_cast<float*>(ws + L.z);
   float* enc = reinterpret_cast<float*>(ws + L.enc);
   float* pooled = reinterpret_cast<float*>(ws + L.pooled);
+  const PoolScratch sc{logits, stats, zpart, z, enc, pooled};
   auto pool = [&](int G, int Sg, float* dst) -> int {
-    const double bytes = 2.0 * M * D * es;  // two streaming passes over the tokens
-    VP_HIP(f.rec(PC_POOL, 2.0 * 2.0 * M * D * NH, bytes, [&] {
-      hipError_t e = pool_logits(feat, bf, M, Sg, D, c->pU, (const bf16_t*)c->pUt, NH, logits, s);
-      if (e != hipSuccess) return e;
-      return pool_softmax_wsum(feat, bf, G, Sg, D, NH, logits, stats, zpart, z, s); }));
-    VP_HIP(small_gemm(z, (int64_t)NH * D, D, c->pWvT, (int64_t)D * dp, c->pbv, dp, enc, (int64_t)NH * dp, dp, G, dp,
-                      D, NH, s));
-    VP_HIP(small_gemm(enc, (int64_t)NH * dp, 0, c->pWpT, 0, c->pbp, 0, pooled, D, 0, G, D, NH * dp, 1, s));
-    VP_HIP(ln_l2_rows(pooled, 0, D, G, D, c->pln_g, c->pln_b, normalize, dst, s));
-    return VP_OK;
+    return run_pooler(f, c->pool, feat, M, G, Sg, D, NH, sc, normalize, dst);
   };
   if ((rc = pool((int)B, S, video_emb))) return rc;
   if (frame_emb && (rc = pool((int)(B * T), N, frame_emb))) return rc;
@@ -421,6 +455,180 @@ int vp_clip_encode_text(vp_clip* c, const int32_t* ids, const float* paddings, i
   // unimodal_ln on the CLS rows, then L2 (encoders.py:752-758, :905-908)
   VP_HIP(ln_l2_rows(static_cast<float*>(x) + (size_t)L * D, 0, (int64_t)(L + 1) * D, (int)Q, D, c->uln_g,
                     c->uln_b, normalize, text_emb, s));
+  return VP_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// FactorizedVideoClassifier (encoders.py:583-653): encoder -> AttenTokenPoolingLayer(hidden D,
+// dim_per_head D/heads, paddings None) -> Dense(num_classes)
+// ------------------------------------------------------------------------------------------
+struct vp_classifier {
+  vp_config cfg;
+  int num_classes = 0;
+  int device = 0;
+  bool finalized = false;
+  vp_handle* video = nullptr;  // 'encoder/' leaves
+  std::map<std::string, vpi::HostParam> host;
+  std::vector<std::string> names;
+  std::map<std::string, std::vector<int64_t>> expected;
+  std::vector<vpi::DevBuf> allocs;
+  bool bf16() const { return cfg.fprop_dtype == VP_BF16; }
+  PoolerW pool;                  // atten_pooler
+  float *wproj = nullptr, *bproj = nullptr;  // projection kernel [D][C] (= Wt of small_gemm), bias [C]
+};
+
+extern "C" {
+
+int vp_classifier_create(const vp_config* cfg, int num_classes, int device, vp_classifier** out) {
+  if (!cfg || !out) return fail(VP_EINVAL, "null argument");
+  *out = nullptr;
+  if (num_classes < 1) return fail(VP_EINVAL, "num_classes must be positive");
+  if (cfg->num_heads > 16) return fail(VP_ENOTSUP, "pooler kernels support up to 16 heads");
+  vp_handle* v = nullptr;
+  int rc = vp_create(cfg, device, &v);
+  if (rc) return rc;
+  v->prefix = "encoder/";
+  v->names.clear();
+  v->expected.clear();
+  build_expected(v);
+  vp_classifier* c = new vp_classifier();
+  c->cfg = *cfg;
+  c->num_classes = num_classes;
+  c->device = device;
+  c->video = v;
+  const int64_t D = cfg->model_dim, NH = cfg->num_heads;
+  add_pooler_expected(c, "atten_pooler/", D, NH, D / NH);
+  add_expected(c, "projection/linear/kernel", {D, (int64_t)num_classes});
+  add_expected(c, "projection/linear/bias", {(int64_t)num_classes});
+  *out = c;
+  return VP_OK;
+}
+
+int vp_classifier_destroy(vp_classifier* c) {
+  if (!c) return VP_OK;
+  vp_destroy(c->video);
+  hipSetDevice(c->device);
+  for (auto& a : c->allocs) hipFree(a.p);
+  delete c;
+  return VP_OK;
+}
+
+int vp_classifier_set_param(vp_classifier* c, const char* name, const float* host_data, const int64_t* shape,
+                            int ndim) {
+  if (!c || !name || !host_data || (ndim > 0 && !shape)) return fail(VP_EINVAL, "null argument");
+  if (c->finalized) return fail(VP_ESTATE, "handle already finalized");
+  if (!std::strncmp(name, "encoder/", 8)) return vp_set_param(c->video, name, host_data, shape, ndim);
+  auto it = c->expected.find(name);
+  if (it == c->expected.end()) return fail(VP_EINVAL, std::string("unexpected parameter: ") + name);
+  const auto& exp = it->second;
+  bool ok = (int)exp.size() == ndim;
+  for (int i = 0; ok && i < ndim; ++i) ok = exp[i] == shape[i];
+  if (!ok) return fail(VP_EINVAL, std::string("shape mismatch for ") + name);
+  size_t n = 1;
+  for (int i = 0; i < ndim; ++i) n *= (size_t)shape[i];
+  HostParam hp;
+  hp.shape.assign(shape, shape + ndim);
+  hp.data.assign(host_data, host_data + n);
+  c->host[name] = std::move(hp);
+  return VP_OK;
+}
+
+int vp_classifier_param_count(const vp_classifier* c, int* count) {
+  if (!c || !count) return fail(VP_EINVAL, "null argument");
+  *count = (int)(c->video->names.size() + c->names.size());
+  return VP_OK;
+}
+
+int vp_classifier_param_name(const vp_classifier* c, int index, const char** name) {
+  if (!c || !name || index < 0) return fail(VP_EINVAL, "bad index");
+  const int nv = (int)c->video->names.size();
+  if (index < nv) {
+    *name = c->video->names[index].c_str();
+    return VP_OK;
+  }
+  if (index - nv >= (int)c->names.size()) return fail(VP_EINVAL, "bad index");
+  *name = c->names[index - nv].c_str();
+  return VP_OK;
+}
+
+int vp_classifier_finalize(vp_classifier* c) {
+  if (!c) return fail(VP_EINVAL, "null handle");
+  if (c->finalized) return VP_OK;
+  for (const auto& n : c->names)
+    if (!c->host.count(n)) return fail(VP_ESTATE, "missing parameter: " + n);
+  int rc = vp_finalize(c->video);
+  if (rc) return rc;
+  VP_HIP(hipSetDevice(c->device));
+  const int64_t D = c->cfg.model_dim, NH = c->cfg.num_heads;
+  if ((rc = pack_pooler(c, "atten_pooler/", D, NH, D / NH, c->pool)) ||
+      (rc = upload_f32(c, param_data(c, "projection/linear/kernel"), &c->wproj)) ||
+      (rc = upload_f32(c, param_data(c, "projection/linear/bias"), &c->bproj)))
+    return rc;
+  c->host.clear();
+  c->finalized = true;
+  return VP_OK;
+}
+
+int vp_classifier_video_handle(vp_classifier* c, vp_handle** video) {
+  if (!c || !video) return fail(VP_EINVAL, "null argument");
+  *video = c->video;
+  return VP_OK;
+}
+
+int vp_classifier_workspace_bytes(const vp_classifier* c, int64_t B, int64_t T, int64_t H, int64_t W,
+                                  size_t* bytes) {
+  if (!c || !bytes) return fail(VP_EINVAL, "null argument");
+  size_t inner = 0;
+  int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
+  if (rc) return rc;
+  const ClipVideoWs L = pool_video_ws(c->cfg, B, T, H, W, inner, c->cfg.model_dim / c->cfg.num_heads);
+  *bytes = L.total + align256((size_t)B * c->cfg.model_dim * 4);
+  return VP_OK;
+}
+
+int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
+                          int64_t W, const float* frame_paddings, float* logits, float* embeddings,
+                          void* spatial_out, void* spatiotemporal_out, int out_dtype, void* workspace,
+                          size_t ws_bytes, void* stream) {
+  using namespace vp;
+  if (!c || !video || !logits || !workspace) return fail(VP_EINVAL, "null argument");
+  if (!c->finalized) return fail(VP_ESTATE, "vp_classifier_finalize has not been called");
+  const bool bf = c->bf16();
+  const int fdt = bf ? VP_BF16 : VP_F32;
+  if (spatiotemporal_out && out_dtype != fdt)
+    return fail(VP_EINVAL, "spatiotemporal_features are returned in the fprop dtype");
+  size_t inner = 0, need = 0;
+  int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
+  if (rc) return rc;
+  const vp_config& v = c->cfg;
+  const int D = v.model_dim, NH = v.num_heads;
+  const ClipVideoWs L = pool_video_ws(v, B, T, H, W, inner, D / NH);
+  if ((rc = vp_classifier_workspace_bytes(c, B, T, H, W, &need))) return rc;
+  if (ws_bytes < need) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(need));
+  const int P = v.patch_size, N = (int)((H / P) * (W / P));
+  const int M = (int)(B * T * N);
+  char* ws = static_cast<char*>(workspace);
+  void* feat = ws + L.feat;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  // 1. encoder -> features [B, T*N, D] (encoders.py:621-630)
+  rc = vp_forward(c->video, video, in_dtype, B, T, H, W, frame_paddings, feat, fdt, spatial_out, ws + L.inner,
+                  inner, stream);
+  if (rc) return rc;
+  VP_HIP(hipSetDevice(c->device));
+  if (spatiotemporal_out)
+    VP_HIP(hipMemcpyAsync(spatiotemporal_out, feat, (size_t)M * D * (bf ? 2 : 4), hipMemcpyDeviceToDevice, s));
+  Fwd f;
+  f.s = s; f.bf = bf; f.M = M; f.D = D; f.NH = NH; f.cap = v.atten_logit_cap;
+  f.pf = &c->video->prof;
+  // 2. atten_pooler over all T*N tokens, paddings None (:634-641); 3. projection (:646-652)
+  float* emb = embeddings ? embeddings : reinterpret_cast<float*>(ws + L.total);
+  const PoolScratch sc{reinterpret_cast<float*>(ws + L.logits), reinterpret_cast<float*>(ws + L.stats),
+                       reinterpret_cast<float*>(ws + L.zpart), reinterpret_cast<float*>(ws + L.z),
+                       reinterpret_cast<float*>(ws + L.enc), reinterpret_cast<float*>(ws + L.pooled)};
+  if ((rc = run_pooler(f, c->pool, feat, M, (int)B, (int)(T * N), D, NH, sc, 0, emb))) return rc;
+  VP_HIP(small_gemm(emb, D, 0, c->wproj, 0, c->bproj, 0, logits, c->num_classes, 0, (int)B, c->num_classes, D, 1, s));
   return VP_OK;
 }
 

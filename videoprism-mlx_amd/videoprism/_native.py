@@ -105,6 +105,19 @@ _SIGNATURES = {
     "vp_clip_encode_video": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64,
                                      c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                      c_void_p, c_size_t, c_void_p]),
+    # FactorizedVideoClassifier
+    "vp_classifier_create": (c_int, [POINTER(vp_config), c_int, c_int, POINTER(c_void_p)]),
+    "vp_classifier_destroy": (c_int, [c_void_p]),
+    "vp_classifier_set_param": (c_int, [c_void_p, c_char_p, c_void_p, POINTER(c_int64), c_int]),
+    "vp_classifier_param_count": (c_int, [c_void_p, POINTER(c_int)]),
+    "vp_classifier_param_name": (c_int, [c_void_p, c_int, POINTER(c_char_p)]),
+    "vp_classifier_finalize": (c_int, [c_void_p]),
+    "vp_classifier_video_handle": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "vp_classifier_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64,
+                                              POINTER(c_size_t)]),
+    "vp_classifier_forward": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                      c_void_p, c_size_t, c_void_p]),
     "vp_clip_text_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_size_t)]),
     "vp_clip_encode_text": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p,
                                     c_void_p, c_size_t, c_void_p]),

@@ -524,3 +524,180 @@ class FactorizedVideoCLIP:
         return video_emb, text_emb, outputs
 
     __call__ = apply
+
+
+class ClassifierEngine:
+    """One vp_classifier handle (FactorizedVideoClassifier weights on one device)."""
+
+    def __init__(self, cfg: dict, num_classes: int, flat_params: dict, device: int, bf16: bool):
+        self.cfg = dict(cfg)
+        self.num_classes = num_classes
+        self.device = device
+        self.bf16 = bf16
+        lib = _native.load()
+        v = _native.vp_config(
+            patch_size=cfg["patch_size"], pos_emb_t=cfg["pos_emb_shape"][0],
+            pos_emb_h=cfg["pos_emb_shape"][1], pos_emb_w=cfg["pos_emb_shape"][2],
+            model_dim=cfg["model_dim"], num_spatial_layers=cfg["num_spatial_layers"],
+            num_temporal_layers=cfg["num_temporal_layers"], num_heads=cfg["num_heads"],
+            mlp_dim=cfg["mlp_dim"], atten_logit_cap=float(cfg.get("atten_logit_cap", 0.0)),
+            fprop_dtype=_native.VP_BF16 if bf16 else _native.VP_F32)
+        h = ctypes.c_void_p()
+        _native.check(lib.vp_classifier_create(ctypes.byref(v), num_classes, device, ctypes.byref(h)))
+        self._h = h
+        try:
+            for name, arr in flat_params.items():
+                a = np.ascontiguousarray(arr, dtype=np.float32)
+                shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+                _native.check(lib.vp_classifier_set_param(h, name.encode(),
+                                                          a.ctypes.data_as(ctypes.c_void_p), shape,
+                                                          a.ndim))
+            _native.check(lib.vp_classifier_finalize(h))
+        except Exception:
+            lib.vp_classifier_destroy(h)
+            self._h = None
+            raise
+        self._ws = None
+        self._grids = set()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _native._lib is not None:
+            _native._lib.vp_classifier_destroy(h)
+            self._h = None
+
+    def video_handle(self):
+        v = ctypes.c_void_p()
+        _native.call("vp_classifier_video_handle", self._h, ctypes.byref(v))
+        return v
+
+    def forward(self, video, frame_paddings=None, want_embeddings=False, want_spatial=False,
+                want_spatiotemporal=False, stream=None):
+        torch = _torch()
+        B, T, H, W, C = video.shape
+        P = self.cfg["patch_size"]
+        if C != 3:
+            raise ValueError("inputs must have 3 channels")
+        if H % P or W % P:
+            raise ValueError(f"Image height ({H}) and width ({W}) should be multiples "
+                             f"of patch_size ({P}).")
+        video = video.contiguous()
+        if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
+            video = video.float()
+        in_dt = _native._prec(video)
+        if (H, W) not in self._grids:
+            _native.call("vp_prepare_geometry", self.video_handle(), H, W)
+            self._grids.add((H, W))
+        D, N = self.cfg["model_dim"], (H // P) * (W // P)
+        dev = video.device
+        fdt = torch.bfloat16 if self.bf16 else torch.float32
+        logits = torch.empty((B, self.num_classes), dtype=torch.float32, device=dev)
+        emb = torch.empty((B, D), dtype=torch.float32, device=dev) if want_embeddings else None
+        sp = torch.empty((B, T * N, D), dtype=fdt, device=dev) if want_spatial else None
+        st = torch.empty((B, T * N, D), dtype=fdt, device=dev) if want_spatiotemporal else None
+        fp = None
+        if frame_paddings is not None:
+            fp = frame_paddings.to(device=dev, dtype=torch.float32).contiguous()
+            if tuple(fp.shape) != (B, T):
+                raise AssertionError(f"frame_paddings.shape == {(B, T)} failed (encoders.py:442)")
+        n = ctypes.c_size_t()
+        _native.call("vp_classifier_workspace_bytes", self._h, B, T, H, W, ctypes.byref(n))
+        if self._ws is None or self._ws.numel() < n.value:
+            self._ws = None
+            self._ws = torch.empty(max(n.value, 256), dtype=torch.uint8, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        _native.call("vp_classifier_forward", self._h, ptr(video), in_dt, B, T, H, W, ptr(fp),
+                     ptr(logits), ptr(emb), ptr(sp), ptr(st),
+                     _native.VP_BF16 if self.bf16 else _native.VP_F32, ptr(self._ws),
+                     self._ws.numel(), ctypes.c_void_p(s.cuda_stream))
+        return logits, emb, sp, st
+
+
+@dataclasses.dataclass
+class FactorizedVideoClassifier:
+    """encoders.py:583-653: `encoder_params` (a FactorizedEncoder config) and `num_classes`."""
+
+    encoder_params: dict = dataclasses.field(default_factory=dict)
+    num_classes: int = 0
+    fprop_dtype: Any = None
+    dtype: Any = None
+
+    def __post_init__(self):
+        self._engines: dict = {}
+
+    @property
+    def is_bf16(self) -> bool:
+        return _is_bf16_dtype(self.fprop_dtype)
+
+    def config(self) -> dict:
+        c = {k: v for k, v in self.encoder_params.items() if k not in ("scan", "norm_policy")}
+        c["pos_emb_shape"] = tuple(c["pos_emb_shape"])
+        return c
+
+    def param_specs(self) -> dict:
+        return params_lib.classifier_leaf_specs(self.config(), self.num_classes, scan=True)
+
+    def init(self, rng=0, inputs=None, train: bool = False, **kwargs) -> dict:
+        del inputs, train, kwargs
+        seed = int(np.asarray(rng).ravel()[-1]) if not isinstance(rng, int) else rng
+        return params_lib.synthetic_params(self.config(), seed, specs=self.param_specs())
+
+    def engine(self, variables, device: int) -> ClassifierEngine:
+        p = variables["params"] if isinstance(variables, dict) and "params" in variables else variables
+        key = (id(p), device, self.is_bf16)
+        ent = self._engines.get(key)
+        if ent is not None and ent[0] is p:
+            return ent[1]
+        if self.encoder_params.get("norm_policy", "pre") != "pre":
+            raise NotImplementedError("only norm_policy='pre' is implemented")
+        flat = params_lib.canonical_params(variables)
+        params_lib.validate(flat, self.param_specs())
+        eng = ClassifierEngine(self.config(), self.num_classes, flat, device, self.is_bf16)
+        self._engines[key] = (p, eng)
+        return eng
+
+    def apply(self, variables, inputs, train: bool = False,
+              return_intermediate: bool | Collection[str] = False, frame_paddings=None, **kwargs):
+        """encoders.py:594-653 -> (logits [B, num_classes], outputs)."""
+        del train
+        if kwargs.get("method") not in (None,):
+            raise NotImplementedError("apply(method=...) is not supported")
+        torch = _torch()
+        as_numpy = not isinstance(inputs, torch.Tensor)
+        if as_numpy:
+            arr = np.asarray(inputs)
+            x = torch.from_numpy(np.ascontiguousarray(
+                arr if arr.dtype == np.uint8 else arr.astype(np.float32, copy=False)))
+            device = torch.cuda.current_device()
+        else:
+            x = inputs
+            device = x.device.index if x.is_cuda else torch.cuda.current_device()
+        x = x.to(f"cuda:{device}")
+        if x.dim() != 5:
+            raise ValueError(f"inputs must be [B, T, H, W, 3], got {tuple(x.shape)}")
+        assert x.shape[2] == x.shape[3]  # encoders.py:435
+        if self.is_bf16 and x.dtype == torch.float32:
+            x = x.to(torch.bfloat16)
+        fp = None
+        if frame_paddings is not None:
+            fp = frame_paddings if isinstance(frame_paddings, torch.Tensor) else \
+                torch.from_numpy(np.asarray(frame_paddings, dtype=np.float32))
+        eng = self.engine(variables, device)
+        logits, emb, sp, st = eng.forward(
+            x, fp, want_embeddings=_contains(return_intermediate, "global_embeddings"),
+            want_spatial=_contains(return_intermediate, "spatial_features"),
+            want_spatiotemporal=_contains(return_intermediate, "spatiotemporal_features"))
+        fdt = torch.bfloat16 if self.is_bf16 else torch.float32
+        logits = logits.to(fdt)
+        outputs = {}
+        for k, v in (("spatial_features", sp), ("spatiotemporal_features", st),
+                     ("global_embeddings", emb)):
+            if v is not None:
+                outputs[k] = v.to(fdt)
+        if as_numpy:
+            logits = logits.float().cpu().numpy()
+            outputs = {k: v.float().cpu().numpy() for k, v in outputs.items()}
+        return logits, outputs
+
+    __call__ = apply

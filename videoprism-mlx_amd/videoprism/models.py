@@ -88,6 +88,22 @@ def videoprism_lvt_v1_large(text_tokenizer: str = "c4_en"):
     return encoders.FactorizedVideoCLIP(**config)
 
 
+def videoprism_vc_v1_base(num_classes: int):
+    """models.py:195-200: FactorizedVideoClassifier on the Base encoder."""
+    return encoders.FactorizedVideoClassifier(encoder_params=dict(CONFIGS["videoprism_v1_base"]),
+                                              num_classes=num_classes)
+
+
+def videoprism_vc_v1_large(num_classes: int):
+    return encoders.FactorizedVideoClassifier(encoder_params=dict(CONFIGS["videoprism_v1_large"]),
+                                              num_classes=num_classes)
+
+
+def videoprism_vc_v1_giant(num_classes: int):
+    return encoders.FactorizedVideoClassifier(encoder_params=dict(CONFIGS["videoprism_v1_giant"]),
+                                              num_classes=num_classes)
+
+
 MODELS = {
     "videoprism_public_v1_base": videoprism_v1_base,
     "videoprism_public_v1_large": videoprism_v1_large,

@@ -134,7 +134,26 @@ def load_model(model_name: str, weights_path: str = None, fprop_dtype=None) -> V
                      fprop_dtype=fprop_dtype)
 
 
-def load_classifier(model_name: str, num_classes: int, weights_path: str = None):
-    """models_mlx.py:213-294: FactorizedVideoClassifier is out of scope."""
-    get_model_config(model_name)
-    raise NotImplementedError("FactorizedVideoClassifier is out of scope for this build")
+def load_classifier(model_name: str, num_classes: int, weights_path: str = None, fprop_dtype=None):
+    """models_mlx.py:213-294: a FactorizedVideoClassifier on the named model's encoder (for LvT
+    names the vision encoder's hyper-parameters).  Pre-trained files hold the encoder only, so the
+    pooler and the projection start from the Flax initialisers' distributions (deterministic numpy
+    draws) -- the reference likewise loads only the encoder weights; returns (model, variables)."""
+    config = get_model_config(model_name)
+    enc = {k: config[k] for k in ("patch_size", "pos_emb_shape", "model_dim", "num_spatial_layers",
+                                  "num_temporal_layers", "num_heads", "mlp_dim", "atten_logit_cap")}
+    model = encoders.FactorizedVideoClassifier(encoder_params=enc, num_classes=num_classes,
+                                               fprop_dtype=fprop_dtype)
+    variables = model.init(0)
+    if weights_path is not None:
+        flat = load_weights_from_file(str(_resolve(model_name, weights_path)))
+        canonical = params_lib.canonical_params(flat)
+        tree = params_lib.flatten(variables["params"])
+        for k, v in canonical.items():
+            k = k[len("vision_encoder/"):] if k.startswith("vision_encoder/") else k
+            k = k[len("encoder/"):] if k.startswith("encoder/") else k
+            key = "encoder/" + k
+            if key in tree:
+                tree[key] = v
+        variables = {"params": params_lib.unflatten(tree)}
+    return model, variables

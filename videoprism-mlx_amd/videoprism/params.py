@@ -113,6 +113,29 @@ def clip_leaf_specs(cfg: dict, scan: bool = True) -> dict[str, tuple[int, ...]]:
     return specs
 
 
+def classifier_leaf_specs(cfg: dict, num_classes: int, scan: bool = True) -> dict[str, tuple[int, ...]]:
+    """FactorizedVideoClassifier (encoders.py:583-653): 'encoder/...', 'atten_pooler/...'
+    (AttenTokenPoolingLayer, hidden D so dim_per_head = D/N) and 'projection/linear/...':
+    54 leaves for a scanned encoder (encoders_test.py:224)."""
+    D = cfg["model_dim"]
+    nh = cfg["num_heads"]
+    dp = D // nh
+    specs = {f"encoder/{k}": v for k, v in encoder_leaf_specs(cfg, scan).items()}
+    pre = "atten_pooler"
+    specs[f"{pre}/pooling_attention_query"] = (1, D)
+    specs[f"{pre}/pooling_attention/per_dim_scale/per_dim_scale"] = (dp,)
+    for q in ("query", "key", "value"):
+        specs[f"{pre}/pooling_attention/{q}/w"] = (D, nh, dp)
+        specs[f"{pre}/pooling_attention/{q}/b"] = (nh, dp)
+    specs[f"{pre}/pooling_attention/post/w"] = (D, nh, dp)
+    specs[f"{pre}/pooling_attention/post/b"] = (D,)
+    specs[f"{pre}/pooling_attention_layer_norm/scale"] = (D,)
+    specs[f"{pre}/pooling_attention_layer_norm/bias"] = (D,)
+    specs["projection/linear/kernel"] = (D, num_classes)
+    specs["projection/linear/bias"] = (num_classes,)
+    return specs
+
+
 def count_params(specs: dict[str, tuple[int, ...]]) -> int:
     return int(sum(int(np.prod(s)) for s in specs.values()))
 
