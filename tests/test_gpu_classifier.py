@@ -34,3 +34,20 @@ def test_classifier_reduced_depth(cuda, bf16):
         assert el < 3e-2 and eg < 1e-3
     else:
         assert el < 2e-5 and np.abs(out["global_embeddings"] - rout["global_embeddings"]).max() < 2e-5
+
+
+def test_classifier_large_u8(cuda):
+    """Large dims (16 heads), uint8 frames, frame paddings; fp32."""
+    enc = dict(models.CONFIGS["videoprism_v1_large"])
+    enc.update(num_spatial_layers=1, num_temporal_layers=1)
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedVideoClassifier(encoder_params=enc,
+                                                                                  num_classes=7))
+    var = params.synthetic_params(enc, 8, specs=m.param_specs())
+    frames = np.random.default_rng(8).integers(0, 256, (1, 3, 288, 288, 3), dtype=np.uint8)
+    fpad = np.array([[0.0, 0.0, 1.0]], np.float32)
+    logits, _ = m.apply(var, frames, frame_paddings=fpad)
+    ref, _ = orc.video_classifier(var["params"], enc, frames.astype(np.float32) / np.float32(255.0),
+                                  frame_paddings=fpad)
+    err = np.abs(logits - ref).max()
+    print(f"classifier Large u8 f32: logits max-abs {err:.3e}")
+    assert err < 2e-5

@@ -166,3 +166,30 @@ def test_clip_apply_api(cuda):
     np.testing.assert_allclose(v, v2, atol=1e-6)
     rv, rt, _ = orc.video_clip(var["params"], cfg, video, ids, pads, "f64")
     assert np.abs(v - rv).max() < 2e-5 and np.abs(t - rt).max() < 2e-5
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_clip_large_dims_padded_frames(cuda, bf16):
+    """LvT-Large dims (D 1024, 16 heads: pooler dh 256 with 2H = 32 logit columns, temporal
+    pos-emb 8 -> T), reduced depth; a padded frame in the vision encoder (the auxiliary
+    encoder and the pooler see no paddings, encoders.py:846-872); out-of-range text ids clamp."""
+    cfg = _lvt_cfg("videoprism_lvt_v1_large", num_spatial_layers=1, num_temporal_layers=1,
+                   num_auxiliary_layers=1, num_unimodal_layers=1)
+    var = params.synthetic_params(cfg, 21, specs=params.clip_leaf_specs(cfg))
+    video = np.random.default_rng(21).random((2, 2, 288, 288, 3), dtype=np.float32)
+    fpad = np.zeros((2, 2), np.float32)
+    fpad[1, 1] = 1.0
+    ids, pads = _text(3, 12, 21, cfg["vocabulary_size"])
+    ids[0, 0] = cfg["vocabulary_size"] + 5   # clamps to V-1, as a JAX gather does
+    ids[1, 1] = -3                           # clamps to 0
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedVideoCLIP(**cfg),
+                         fprop_dtype=torch.bfloat16 if bf16 else None)
+    v, t, out = m.apply(var, video, ids, pads, frame_paddings=fpad,
+                        return_intermediate=("frame_embeddings",))
+    rv, rt, rout = orc.video_clip(var["params"], cfg, video, ids, pads, "f64",
+                                  return_intermediate=("frame_embeddings",), frame_paddings=fpad)
+    ev, et = np.abs(v - rv).max(), np.abs(t - rt).max()
+    ef = np.abs(out["frame_embeddings"] - rout["frame_embeddings"]).max()
+    print(f"LvT-L dims {'bf16' if bf16 else 'f32'}: video {ev:.3e} frames {ef:.3e} text {et:.3e}")
+    tol = 2e-3 if bf16 else 2e-5   # bf16 outputs are returned in bf16 (2^-9 relative)
+    assert ev <= tol and ef <= tol and et <= tol, (ev, ef, et)
