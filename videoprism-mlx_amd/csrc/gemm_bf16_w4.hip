@@ -55,7 +55,8 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // without its global stores (LDS transposition and math kept), 64 = start skew: workgroup
 // group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
 // K-tile, so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
-// schedule with the 16 loads and 16 reads in its first 32 MFMAs, 256 = plain (temporal) output stores.
+// schedule with the 16 loads and 16 reads in its first 32 MFMAs, 256 = plain (temporal) output stores,
+// 512 (production) = no padded rows: the epilogue skips the (1 - rowpad) factor.
 // PF > 0: L2 prefetch of A, PF K-tiles beyond the K-tile being staged (one dword per A row per
 // K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  Pays where A streams
 // from HBM (ffn_layer2, K = 3072: 490 -> 471 us); costs on the K = 768 shapes (A mostly from the
@@ -355,14 +356,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
         }
         float keep = 1.0f;
-        if constexpr (Tr::kKeep) {
+        if constexpr (Tr::kKeep && !(DIAG & 512)) {
           if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
         }
         if constexpr (DIAG & 32) {
           if (ep.ldo == -12345) epi_store8<EPI>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
           else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
         } else {
-          const epi_u32x4 pk = epi_store8<EPI, !(DIAG & 256)>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          const epi_u32x4 pk =
+              epi_store8<EPI, !(DIAG & 256), !(DIAG & 512)>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
           if constexpr (Tr::kStats) {
             float y[8];
 #pragma unroll
@@ -438,7 +440,7 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
 namespace {
 // production epilogues; D = 0: nontemporal output stores, D = 256: plain stores (ablation)
 template <int D>
-hipError_t w4_dispatch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
+hipError_t w4_dispatch_d(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                        int K, const EpiArgs& ep, hipStream_t s) {
   switch (epi) {
     case EPI_BF16: return launch_w4<EPI_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
@@ -461,6 +463,17 @@ hipError_t w4_dispatch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, i
     case EPI_RELU_BF16: return launch_w4<EPI_RELU_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
+}
+// ffn_layer1 launches without padded rows take the no-(1 - rowpad) build of the GELU epilogue
+// (bitwise equal; ffn1 11.0-11.26 -> 10.9-11.0 ms/step).  The same build of the residual epilogues
+// measured slower (post 2.78 -> 3.0, ffn2 7.87 -> 8.1 ms/step: different schedules), so they keep
+// the multiply.
+template <int D>
+hipError_t w4_dispatch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
+                       int K, const EpiArgs& ep, hipStream_t s) {
+  if (!ep.rowpad && epi == EPI_GELU_BF16_LN)
+    return launch_w4<EPI_GELU_BF16_LN, D | 512>(A, lda, W, ldw, M, N, K, ep, s);
+  return w4_dispatch_d<D>(epi, A, lda, W, ldw, M, N, K, ep, s);
 }
 }  // namespace
 
@@ -488,6 +501,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 1024: return launch_w4<EPI_BF16, 0, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 2048: return launch_w4<EPI_BF16, 0, 3>(A, lda, W, ldw, M, N, K, ep, s);
       case 4096: return launch_w4<EPI_BF16, 0, 4>(A, lda, W, ldw, M, N, K, ep, s);
+      // ffn_layer1 epilogue with the (1 - rowpad) multiply kept (A/B of the DIAG 512 build)
+      case 2009: return launch_w4<EPI_GELU_BF16_LN, 0>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
   }

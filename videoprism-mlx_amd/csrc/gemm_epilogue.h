@@ -153,11 +153,13 @@ typedef unsigned epi_u32x4 __attribute__((ext_vector_type(4)));
 // encoder's shapes in isolation: qkv 432 -> 379 us, post 147 -> 130 us, ffn1 579 -> 502 us
 // (tools/gemm_bench.py nt); inside the full forward within +-1 %.
 // returns the stored bf16 values (packed) for the row-statistics epilogues
-template <int EPI, bool NT = true>
+// KEEP = false: the launch has no padded rows (rowpad == nullptr), so the (1 - rowpad) factor is
+// skipped -- bitwise the same result, one packed multiply per value pair less
+template <int EPI, bool NT = true, bool KEEP = true>
 __device__ __forceinline__ epi_u32x4 epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
   using Tr = EpiTraits<EPI>;
-  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep, Tr::kExtra, Tr::kRelu);
-  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep, Tr::kExtra, Tr::kRelu);
+  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep && KEEP, Tr::kExtra, Tr::kRelu);
+  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep && KEEP, Tr::kExtra, Tr::kRelu);
   epi_u32x4 pk = {0u, 0u, 0u, 0u};
   if constexpr (Tr::kOutBf16) {
     pk = epi_u32x4{pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
