@@ -28,16 +28,21 @@ def main():
     f2 = lambda: nat.dev_gemm_ln(a, w, b, nat.EPI_GELU_LN, o2, rowpad=zero_pad, ln_rs=rs, ln_c=c)  # noqa: E731
     o3 = torch.empty_like(o1)
     f3 = lambda: nat.dev_gemm_ln(a, w, b, 3009, o3, ln_rs=rs, ln_c=c)  # noqa: E731
+    o4 = torch.empty_like(o1)
+    f4 = lambda: nat.dev_gemm_ln(a, w, b, 3010, o4, ln_rs=rs, ln_c=c)  # noqa: E731
     f1()
     f2()
     f3()
+    f4()
     torch.cuda.synchronize()
-    print("bitwise equal:", bool(torch.equal(o1, o2)), bool(torch.equal(o1, o3)))
-    r1, r2, r3 = [], [], []
+    print("bitwise equal:", bool(torch.equal(o1, o2)), bool(torch.equal(o1, o3)), bool(torch.equal(o1, o4)))
+    r1, r2, r3, r4 = [], [], [], []
     for _ in range(5):
         r1.append(timeit(f1))
         r2.append(timeit(f2))
         r3.append(timeit(f3))
+        r4.append(timeit(f4))
+    print(f"scalar GELU: {min(r4)*1e3:.1f} us")
     print(f"ffn1 GELU+LN epilogue: no-rowpad build {min(r1)*1e3:.1f} us   rowpad multiply (NULL) "
           f"{min(r3)*1e3:.1f} us   zero rowpad array {min(r2)*1e3:.1f} us")
 

@@ -56,7 +56,8 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
 // K-tile, so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
 // schedule with the 16 loads and 16 reads in its first 32 MFMAs, 256 = plain (temporal) output stores,
-// 512 (production) = no padded rows: the epilogue skips the (1 - rowpad) factor.
+// 512 (production) = no padded rows: the epilogue skips the (1 - rowpad) factor, 1024 = GELU in
+// unpacked fp32 arithmetic (A/B).
 // PF > 0: L2 prefetch of A, PF K-tiles beyond the K-tile being staged (one dword per A row per
 // K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  Pays where A streams
 // from HBM (ffn_layer2, K = 3072: 490 -> 471 us); costs on the K = 768 shapes (A mostly from the
@@ -364,7 +365,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           else asm volatile("" :: "v"(v.lo.x), "v"(v.lo.y), "v"(v.lo.z), "v"(v.lo.w), "v"(v.hi.x), "v"(v.hi.y), "v"(v.hi.z), "v"(v.hi.w));
         } else {
           const epi_u32x4 pk =
-              epi_store8<EPI, !(DIAG & 256), !(DIAG & 512)>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+              epi_store8<EPI, !(DIAG & 256), !(DIAG & 512), (DIAG & 1024) != 0>(ep, row, n, v, keep,
+                                                                                   ex[mt & 1][nh][pass]);
           if constexpr (Tr::kStats) {
             float y[8];
 #pragma unroll
@@ -503,6 +505,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 4096: return launch_w4<EPI_BF16, 0, 4>(A, lda, W, ldw, M, N, K, ep, s);
       // ffn_layer1 epilogue with the (1 - rowpad) multiply kept (A/B of the DIAG 512 build)
       case 2009: return launch_w4<EPI_GELU_BF16_LN, 0>(A, lda, W, ldw, M, N, K, ep, s);
+      // + scalar (unpacked) GELU arithmetic
+      case 2010: return launch_w4<EPI_GELU_BF16_LN, 512 | 1024>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
   }

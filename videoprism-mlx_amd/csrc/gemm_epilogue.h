@@ -139,8 +139,9 @@ __device__ __forceinline__ F8 epi_extra8(const EpiArgs& ep, int row, int n, int 
 }
 
 __device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, bool gelu, bool kp, bool ex,
-                                           bool relu = false) {
-  if (gelu) v = gelu4(v);
+                                           bool relu = false, bool scalar_gelu = false) {
+  if (gelu && scalar_gelu) v = make_float4(gelu_fast(v.x), gelu_fast(v.y), gelu_fast(v.z), gelu_fast(v.w));
+  else if (gelu) v = gelu4(v);
   if (relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
   if (kp) { v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep; }
   if (ex) { v.x += extra.x; v.y += extra.y; v.z += extra.z; v.w += extra.w; }
@@ -155,11 +156,11 @@ typedef unsigned epi_u32x4 __attribute__((ext_vector_type(4)));
 // returns the stored bf16 values (packed) for the row-statistics epilogues
 // KEEP = false: the launch has no padded rows (rowpad == nullptr), so the (1 - rowpad) factor is
 // skipped -- bitwise the same result, one packed multiply per value pair less
-template <int EPI, bool NT = true, bool KEEP = true>
+template <int EPI, bool NT = true, bool KEEP = true, bool SCALAR_GELU = false>
 __device__ __forceinline__ epi_u32x4 epi_store8(const EpiArgs& ep, int row, int n, F8 v, float keep, F8 extra) {
   using Tr = EpiTraits<EPI>;
-  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep && KEEP, Tr::kExtra, Tr::kRelu);
-  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep && KEEP, Tr::kExtra, Tr::kRelu);
+  v.lo = epi_math4(v.lo, keep, extra.lo, Tr::kGelu, Tr::kKeep && KEEP, Tr::kExtra, Tr::kRelu, SCALAR_GELU);
+  v.hi = epi_math4(v.hi, keep, extra.hi, Tr::kGelu, Tr::kKeep && KEEP, Tr::kExtra, Tr::kRelu, SCALAR_GELU);
   epi_u32x4 pk = {0u, 0u, 0u, 0u};
   if constexpr (Tr::kOutBf16) {
     pk = epi_u32x4{pack_bf16x2(v.lo.x, v.lo.y), pack_bf16x2(v.lo.z, v.lo.w), pack_bf16x2(v.hi.x, v.hi.y),
