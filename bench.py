@@ -1,20 +1,28 @@
 #!/usr/bin/env python3
 """VideoPrism-Base bf16 forward throughput on MI355X (BASELINE.json metric/configs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload base|large|lvt_large|lvt_base]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one forward of the `videoprism_public_v1_base` FactorizedEncoder (bf16, random-init
 weights of the real architecture) over B=32 synthetic clips [32,16,288,288,3] uniform[0,1)
-already resident in HBM (configs[1]); for N>1 every rank runs its own 32 clips (weak
-scaling, configs[3]: B=32*N) and the step includes the RCCL all-gather of the pooled,
-L2-normalised clip embeddings.  value = clips processed by all ranks / max-over-ranks time.
+already resident in HBM (configs[1]); for N>1 every rank runs its own 32 clips (weak scaling,
+configs[3]: B=32*N) and the step includes the all-gather of the pooled, L2-normalised clip
+embeddings through the library's RCCL collective (vp_allgather).  value = clips processed by all
+ranks / max-over-ranks time.  Without torch.distributed.run, `--gpus N > 1` spawns the N ranks
+itself (before any GPU call in the parent).
 
 Also reported (one JSON line on rank 0):
   roofline     the dominant kernel's algorithmic FLOP (or byte) rate, from HIP events recorded
-               on its launch stream inside the timed region, against the MI355X dense peak
+               on its launch stream inside the timed region, against the MI355X dense peak; its
+               HBM `traffic` from a PMC record of the same kernel symbol and the same sources
+               (profiles/traffic_r02_<workload>.json, tools/pmc_traffic.sh), else null
   cpu_baseline the NumPy oracle (oracle/, fp32) on one clip on this host's cores (rank 0, N=1)
+
+`--standin` replaces the GPU forward by a small CPU function (gloo backend) so the multi-process
+plumbing -- spawning, sharding, the gather's row order, the similarity shape, n_gpus -- can be
+exercised on a machine without GPUs (tests/test_distributed_cpu.py).  It measures nothing.
 """
 
 from __future__ import annotations
@@ -22,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +40,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip parameters)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (same table)
+CPU_BASELINE_THREADS = 16   # the GPU box's CPU share per GPU
 
 
 def gflop_per_clip(cfg: dict, T: int = 16, N: int = 256) -> float:
@@ -72,33 +83,118 @@ WORKLOADS = {
 
 
 def cpu_baseline(cfg, variables) -> dict:
-    """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip — a reported baseline only."""
+    """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip — a reported baseline only.  BLAS
+    threads pinned to CPU_BASELINE_THREADS (the box's CPU share per GPU)."""
     import numpy as np
-    from threadpoolctl import threadpool_info
+    from threadpoolctl import threadpool_info, threadpool_limits
 
     from oracle import videoprism_oracle as orc
     rng = np.random.default_rng(0)
     video = rng.random((1, 16, 288, 288, 3), dtype=np.float32)
-    t0 = time.perf_counter()
-    orc.factorized_encoder(variables["params"], video, cfg, mode="f32")
-    dt = time.perf_counter() - t0
-    threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    with threadpool_limits(limits=CPU_BASELINE_THREADS):
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+        t0 = time.perf_counter()
+        orc.factorized_encoder(variables["params"], video, cfg, mode="f32")
+        dt = time.perf_counter() - t0
     return {"value": round(1.0 / dt, 5), "unit": "clips/s", "cores": int(threads), "kind": "port",
-            "sample": f"1 clip [1,16,288,288,3], full videoprism_public_v1_base forward, NumPy fp32 "
-                      f"oracle (oracle/videoprism_oracle.py), {dt:.1f} s; host has "
-                      f"{len(os.sched_getaffinity(0))} schedulable CPUs"}
+            "sample": f"1 clip [1,16,288,288,3], full {cfg.get('_name', 'model')} forward, NumPy fp32 "
+                      f"oracle (oracle/videoprism_oracle.py), {dt:.1f} s with BLAS pinned to "
+                      f"{threads} threads; the host exposes {len(os.sched_getaffinity(0))} "
+                      f"schedulable CPUs"}
 
 
-def load_traffic(path: str, kernel: str):
+def load_traffic(path: str, symbol: str, workload: str, src_hash: str):
+    """PMC HBM bytes per launch of kernel `symbol` from a traffic record (tools/pmc_summary.py
+    --json) -- only when the record was measured on the same sources and workload."""
     try:
         with open(path) as f:
             t = json.load(f)
     except (OSError, ValueError):
         return None, None
-    k = t.get("kernels", {}).get(kernel)
+    if t.get("src_hash") != src_hash or t.get("workload") != workload:
+        return None, None
+    k = t.get("kernels", {}).get(symbol)
     if not k:
         return None, None
     return k.get("hbm_bytes_per_launch"), t.get("source")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N without a launcher: N child processes of this script (RANK/LOCAL_RANK/WORLD_SIZE/
+    MASTER_ADDR/MASTER_PORT set), started before this parent touches any GPU.  Returns the first
+    non-zero exit code (0 if all ranks succeeded)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c != 0), 0)
+
+
+# ------------------------------------------------------------------------------------------
+# the step's operations: the HIP library (GpuOps) or the CPU stand-in (StandinOps, --standin)
+# ------------------------------------------------------------------------------------------
+class GpuOps:
+    def __init__(self, eng, native):
+        self.eng, self.nat = eng, native
+
+    def forward(self, video, out):
+        self.eng.forward(video, out=out)
+
+    def pool_l2(self, out):
+        return self.nat.op_pool_l2(out)
+
+    def encode_video(self, video):
+        return self.eng.encode_video(video)[0]
+
+    def encode_text(self, ids, pad):
+        return self.eng.encode_text(ids, pad)
+
+    def similarity(self, v, t):
+        return self.nat.op_similarity(v, t)
+
+
+class StandinOps:
+    """CPU stand-in for the multi-process plumbing test: out[b, l, d] = cos(c_b + d / D) with c_b
+    the clip's first pixel (the bench fills clip b of rank r with its global index), so every
+    gathered row names the clip it came from.  Not a measurement."""
+
+    def __init__(self, D: int):
+        self.D = D
+
+    def _emb(self, video):
+        import torch
+        c = video[:, 0, 0, 0, 0].double()
+        return torch.cos(c[:, None] + torch.arange(self.D, dtype=torch.float64)[None, :] / self.D)
+
+    def forward(self, video, out):
+        out.copy_(self._emb(video)[:, None, :].expand_as(out))
+
+    def pool_l2(self, out):
+        m = out.double().mean(dim=1)
+        return (m / m.norm(dim=1, keepdim=True)).float()
+
+    def encode_video(self, video):
+        e = self._emb(video)
+        return (e / e.norm(dim=1, keepdim=True)).float()
+
+    def encode_text(self, ids, pad):
+        import torch
+        e = torch.sin(ids[:, :1].double() + torch.arange(self.D, dtype=torch.float64)[None, :])
+        return (e / e.norm(dim=1, keepdim=True)).float()
+
+    def similarity(self, v, t):
+        return v @ t.T
 
 
 def main() -> None:
@@ -115,34 +211,52 @@ def main() -> None:
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01_v4.json"))
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic record (default profiles/traffic_r02_<workload>.json)")
+    ap.add_argument("--standin", action="store_true",
+                    help="CPU stand-in forward over gloo: multi-process plumbing test, no measurement")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
 
     from videoprism import _native, distributed, models, params
 
-    rank, local_rank, world = distributed.init("nccl")
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
-
+    rank, local_rank, world = distributed.init("gloo" if args.standin else "nccl")
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     name, cfg_key, default_b = WORKLOADS[args.workload]
     lvt = args.workload.startswith("lvt")
     cfg = dict(models.CONFIGS[cfg_key])
-    model = models.get_model(name, fprop_dtype=torch.bfloat16)
-    if lvt:
-        cfg["vocabulary_size"] = model.vocabulary_size
-        variables = params.synthetic_params(cfg, seed=0, specs=params.clip_leaf_specs(cfg))
-    else:
-        variables = params.synthetic_params(cfg, seed=0)
-    eng = model.engine(variables, local_rank)
-
     B, T = args.batch or default_b, args.frames
-    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev).to(torch.bfloat16)
     gather = world > 1 and not args.no_allgather
+    if args.standin:
+        dev = torch.device("cpu")
+        ops = StandinOps(cfg["model_dim"])
+        video = (rank * B + torch.arange(B, dtype=torch.float32))[:, None, None, None, None].expand(
+            B, T, 288, 288, 3).contiguous()
+        comm, eng = None, None
+        if lvt:
+            cfg["vocabulary_size"] = 32000
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device(f"cuda:{local_rank}")
+        model = models.get_model(name, fprop_dtype=torch.bfloat16)
+        if lvt:
+            cfg["vocabulary_size"] = model.vocabulary_size
+            variables = params.synthetic_params(cfg, seed=0, specs=params.clip_leaf_specs(cfg))
+        else:
+            variables = params.synthetic_params(cfg, seed=0)
+        eng = model.engine(variables, local_rank)
+        ops = GpuOps(eng, _native)
+        gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+        video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev).to(torch.bfloat16)
+        comm = distributed.Communicator(local_rank) if gather else None
+
+    last = {}
     if lvt:
         # configs[4]: text ids randint(0, V) [Q, 64] with the second half of every other query
         # padded (models_test.py:61-69), replicated on every rank
@@ -154,28 +268,30 @@ def main() -> None:
         tpad[1::2, Lt // 2:] = 1.0
 
         def step():
-            vemb = eng.encode_video(video)[0]
+            vemb = ops.encode_video(video)
             if gather:
-                vemb = distributed.all_gather_rows(vemb, world)
-            temb = eng.encode_text(ids, tpad)
-            _native.op_similarity(vemb, temb)
+                vemb = distributed.all_gather_rows(vemb, world, comm)
+            temb = ops.encode_text(ids, tpad)
+            last["rows"], last["sim"] = vemb, ops.similarity(vemb, temb)
     else:
-        out = torch.empty((B, T * 256, cfg["model_dim"]), dtype=torch.bfloat16, device=dev)
+        out = torch.empty((B, T * 256, cfg["model_dim"]),
+                          dtype=torch.float32 if args.standin else torch.bfloat16, device=dev)
 
         def step():
-            eng.forward(video, out=out)
+            ops.forward(video, out)
             if gather:
-                pooled = _native.op_pool_l2(out)
-                distributed.all_gather_rows(pooled, world)
+                last["rows"] = distributed.all_gather_rows(ops.pool_l2(out), world, comm)
 
+    sync = (lambda: None) if args.standin else torch.cuda.synchronize
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     launches_per_fwd = 3 + 7 * (cfg["num_spatial_layers"] + cfg["num_temporal_layers"]) + 2
     if lvt:
         launches_per_fwd += 8 * cfg["num_auxiliary_layers"] + 4 + 8 * cfg["num_unimodal_layers"] + 8
-    breakdown, dom_name = {}, None
-    if not args.no_profile:
+    profile = not (args.no_profile or args.standin)
+    breakdown, dom_name, dom_symbol = {}, None, None
+    if profile:
         # per-class breakdown from one extra profiled step outside the timed region (an event
         # pair around every launch costs the stream ~2 %); the timed region then carries events
         # around the dominant class's launches only, for the live roofline
@@ -184,18 +300,19 @@ def main() -> None:
         step()
         breakdown = eng.profile_read()
         dom_name = max(breakdown.items(), key=lambda kv: kv[1]["ms"])[0]
+        dom_symbol = eng.kernel_name(dom_name)
         eng.profile_only([dom_name])
         eng.profile_enable(args.steps * launches_per_fwd + 16)
-    distributed.barrier(dev)
-    torch.cuda.synchronize()
+    distributed.barrier(None if args.standin else dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
-    distributed.barrier(dev)
-    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, dev)
-    prof = eng.profile_read() if not args.no_profile else {}
-    if not args.no_profile:
+    sync()
+    distributed.barrier(None if args.standin else dev)
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, None if args.standin else dev)
+    prof = eng.profile_read() if profile else {}
+    if profile:
         eng.profile_enable(0)
 
     clips = world * B * args.steps
@@ -211,7 +328,8 @@ def main() -> None:
                      sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
         dom = prof[dom_name]
         avg_s = dom["ms"] / dom["launches"] / 1e3
-        traffic, tsrc = load_traffic(args.traffic, dom_name)
+        tpath = args.traffic or os.path.join(ROOT, "profiles", f"traffic_r02_{args.workload}.json")
+        traffic, tsrc = load_traffic(tpath, dom_symbol, args.workload, _native.source_fingerprint())
         if dom["flops"] > 0:
             ach = dom["flops"] / dom["launches"] / avg_s / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
@@ -221,14 +339,30 @@ def main() -> None:
             ach = dom["bytes"] / dom["launches"] / avg_s / 1e9
             roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                         "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic}
-        roofline.update({"kernel": dom_name, "launches": int(dom["launches"]),
+        roofline.update({"kernel": dom_name, "kernel_symbol": dom_symbol,
+                         "launches": int(dom["launches"]),
                          "avg_launch_us": round(avg_s * 1e6, 2),
                          "algorithmic_per_launch": dom["flops"] / dom["launches"] if dom["flops"]
-                         else dom["bytes"] / dom["launches"], "traffic_source": tsrc})
+                         else dom["bytes"] / dom["launches"],
+                         "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
+                         "traffic_source": tsrc})
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not lvt:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not lvt and not args.standin:
+        cfg["_name"] = name
         cpu = cpu_baseline(cfg, variables)
+
+    standin_check = None
+    if args.standin:
+        rows = last.get("rows")
+        expect = StandinOps(cfg["model_dim"])
+        ids_all = torch.arange(world * B, dtype=torch.float32)[:, None, None, None, None]
+        ref = (expect.encode_video(ids_all) if lvt else
+               expect.pool_l2(expect._emb(ids_all)[:, None, :].float()))
+        standin_check = {"gathered_shape": list(rows.shape) if rows is not None else None,
+                         "row_order_ok": bool(rows is not None and rows.shape == ref.shape and
+                                              torch.allclose(rows, ref, atol=1e-6)),
+                         "similarity_shape": list(last["sim"].shape) if "sim" in last else None}
 
     if rank == 0:
         label = {"base": "VideoPrism-Base fwd", "large": "VideoPrism-Large fwd",
@@ -237,7 +371,8 @@ def main() -> None:
         wl = (f"{name} bf16 forward, B={B} clips/GPU x {world} GPU, {T}x288x288x3"
               + (f", {args.queries} text queries x 64 tokens, gathered video_emb @ text_emb.T"
                  if lvt else "")
-              + (", RCCL all-gather of pooled embeddings" if gather else ""))
+              + ((", gloo all-gather (stand-in)" if args.standin else
+                  ", RCCL all-gather (vp_allgather) of pooled embeddings") if gather else ""))
         line = {
             "metric": f"clips/sec (16x288x288) {label}; % MFMA peak",
             "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
@@ -257,8 +392,13 @@ def main() -> None:
             "kernel_ms_per_step_source": "HIP events around every launch of one extra step after "
                                          "warmup (outside the timed region)",
         }
+        if args.standin:
+            line.update({"data": "CPU stand-in forward (--standin): plumbing test, not a measurement",
+                         "dtype": "f32", "standin_check": standin_check})
         print(json.dumps(line), flush=True)
 
+    if comm is not None:
+        comm.close()
     import torch.distributed as dist
     if dist.is_initialized():
         dist.destroy_process_group()

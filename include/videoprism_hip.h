@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VP_ABI_VERSION 3
+#define VP_ABI_VERSION 4
 
 typedef struct vp_handle vp_handle;
 
@@ -45,6 +45,7 @@ enum vp_status {
   VP_EHIP = 3,     /* HIP runtime error */
   VP_ESTATE = 4,   /* handle not finalized / parameter missing */
   VP_ENOTSUP = 5,  /* valid for the reference but outside this library's kernels */
+  VP_ECOMM = 6,    /* RCCL error (vp_comm_*, vp_allgather) */
 };
 
 /* VP_U8: video frames as uint8 [0, 255], normalised in the patchify kernel exactly as
@@ -121,6 +122,10 @@ int vp_profile_read(vp_handle* h, int nclass, double* ms, double* flops, double*
 int vp_profile_set_mask(vp_handle* h, uint32_t class_mask);
 int vp_profile_class_count(void);
 int vp_profile_class_name(int cls, const char** name);
+/* Demangled symbol of the kernel most recently launched for class `cls` on this handle ("" if
+ * none yet), e.g. "void vp::(anonymous namespace)::gemm_bf16_w4_kernel<9, 512, 0>(...)": bench.py
+ * matches PMC traffic records to exactly this kernel.  Valid until the next call for `cls`. */
+int vp_profile_kernel_name(vp_handle* h, int cls, const char** name);
 
 /* ---------------- op-level entry points (kernel parity tests, benches) ---------------- */
 
@@ -247,6 +252,23 @@ int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int
                           int64_t H, int64_t W, const float* frame_paddings, float* logits,
                           float* embeddings, void* spatial_out, void* spatiotemporal_out,
                           int out_dtype, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------- multi-GPU: RCCL all-gather of pooled clip embeddings ----------------
+ * The reference runs on one device; its video-text usage scores every clip against every query,
+ * `similarities = video_emb @ text_emb.T` (README.md:81, verify_clip_models.py:84).  With clips
+ * sharded by batch over one process per GPU, that step needs every rank's
+ * [b, D] video embeddings on every rank: one all-gather over xGMI.  The communicator is RCCL's:
+ * rank 0 creates a unique id (vp_comm_unique_id, vp_comm_id_bytes() bytes), the host sends it to
+ * every rank by any channel (videoprism/distributed.py uses torch.distributed), and every rank
+ * calls vp_comm_init with it (collective: blocks until all nranks joined).
+ * vp_allgather: recv[r*count .. (r+1)*count) = rank r's send[0 .. count) on every rank, dtype
+ * VP_F32 / VP_BF16 / VP_U8, asynchronous on `stream` (device pointers of the comm's device). */
+typedef struct vp_comm vp_comm;
+int vp_comm_id_bytes(void);
+int vp_comm_unique_id(uint8_t* id_out, int64_t nbytes);
+int vp_comm_init(const uint8_t* id, int64_t nbytes, int nranks, int rank, int device, vp_comm** out);
+int vp_comm_destroy(vp_comm* c);
+int vp_allgather(vp_comm* c, const void* send, void* recv, int64_t count, int dtype, void* stream);
 
 #ifdef __cplusplus
 }

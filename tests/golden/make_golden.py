@@ -99,11 +99,45 @@ def g5_clip_tiny():
     np.savez_compressed(os.path.join(HERE, "g5_clip_tiny.npz"), **arrays)
 
 
+# full-depth models at the metric's clip length (configs[1] / configs[2]): the oracle in fp64 and
+# in its emulation of the reference's bf16 graph, on clip 0 of the GPU tests' batches.  Stored:
+# the L2-normalised token-mean ("pooled") vector, every 64th token row, and the inputs' seeds
+# (the GPU tests regenerate the identical video and weights from them).
+FULL = {"g6_base_t16": ("videoprism_v1_base", 0, 11), "g7_large_t16": ("videoprism_v1_large", 0, 12)}
+
+
+def full_video(seed, T=16):
+    return np.random.default_rng(seed).random((1, T, 288, 288, 3), dtype=np.float32)
+
+
+def g_full(tag):
+    name, pseed, vseed = FULL[tag]
+    cfg = models.CONFIGS[name]
+    var = params.synthetic_params(cfg, seed=pseed)
+    x = full_video(vseed)
+    arrays = dict(param_seed=np.array(pseed), video_seed=np.array(vseed), model=np.array(name))
+    for mode in ("f64", "bf16"):
+        e, _ = orc.factorized_encoder(var["params"], x, cfg, mode)
+        m = e.astype(np.float64).mean(axis=1)
+        arrays[f"pooled_{mode}"] = m / np.sqrt((m * m).sum(-1, keepdims=True) + 1e-12)
+        arrays[f"rows_{mode}"] = e[0, ::64].astype(np.float32)
+        arrays[f"frame_mean_{mode}"] = e[0].reshape(16, -1, e.shape[-1]).mean(axis=1).astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **arrays)
+
+
 if __name__ == "__main__":
-    g1_tiny()
-    g2_base_dims()
-    g4_ops()
-    g5_clip_tiny()
+    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7"]
+    if "g1" in which:
+        g1_tiny()
+    if "g2" in which:
+        g2_base_dims()
+    if "g4" in which:
+        g4_ops()
+    if "g5" in which:
+        g5_clip_tiny()
+    for tag in FULL:
+        if tag[:2] in which:
+            g_full(tag)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

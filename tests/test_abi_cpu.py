@@ -22,7 +22,29 @@ def header_symbols():
 def test_library_present_and_loads():
     assert os.path.exists(_native.library_path()), "build with __graft_entry__.build()"
     lib = _native.load()
-    assert lib.vp_abi_version() == 3
+    want = int(re.search(r"#define VP_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert lib.vp_abi_version() == want
+
+
+def test_product_library_has_no_ablation_builds():
+    """The A/B and ablation kernels live in the tools' diag library only (make diag): the product
+    library exports no diag entry points and reads no kernel-selection environment switch."""
+    lib = ctypes.CDLL(_native.library_path())
+    for sym in ("vp_dev_gemm_diag", "vp_dev_attention_diag"):
+        assert not hasattr(lib, sym), sym
+    blob = open(_native.library_path(), "rb").read()
+    assert b"VP_GEMM_KERNEL" not in blob and b"gemm_bf16_ov" not in blob
+
+
+def test_comm_entry_points_without_a_gpu():
+    """vp_comm_*: id size and argument checks (no RCCL call is made for bad arguments)."""
+    lib = _native.load()
+    assert lib.vp_comm_id_bytes() == 128
+    h = ctypes.c_void_p()
+    uid = (ctypes.c_uint8 * 128)()
+    assert lib.vp_comm_init(uid, 128, 2, 5, 0, ctypes.byref(h)) == _native.VP_EINVAL
+    assert lib.vp_comm_init(uid, 16, 2, 0, 0, ctypes.byref(h)) == _native.VP_EINVAL
+    assert lib.vp_allgather(None, None, None, 1, 0, None) == _native.VP_EINVAL
 
 
 def test_every_header_symbol_exported():

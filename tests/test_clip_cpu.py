@@ -171,3 +171,64 @@ def test_oracle_classifier_vs_torch_restatement():
     x = np.random.default_rng(3).normal(0, 0.1, (2, 4, 16, 16, 3)).astype(np.float32)
     logits, _ = orc.video_classifier(var["params"], ENC_TINY, x)
     np.testing.assert_allclose(logits, torch_restatement.video_classifier(var["params"], ENC_TINY, x), atol=1e-11)
+
+
+def _convert_like_reference(flat: dict, cfg: dict, lvt: bool) -> dict:
+    """Restates convert_weights.py:88-104 (rename_parameter) and :107-226 (convert_flax_to_mlx):
+    scanned stacks listed by component are unstacked to `<prefix>/layers/{i}/...` (only when
+    dim 0 == the component's layer count), then '/kernel', '/scale', '/emb_var' -> '/weight'
+    everywhere.  Test-side restatement; the reference script itself needs flax."""
+    def rename(n):
+        return n.replace("/kernel", "/weight").replace("/scale", "/weight").replace("/emb_var", "/weight")
+    vp = "vision_encoder/" if lvt else ""
+    comps = [(f"{vp}spatial_encoder/transformers_stack", cfg["num_spatial_layers"]),
+             (f"{vp}temporal_encoder/transformers_stack", cfg["num_temporal_layers"])]
+    if lvt:
+        comps += [("text_encoder/unimodal_transformer", cfg["num_unimodal_layers"]),
+                  ("auxiliary_encoder/transformers_stack", cfg["num_auxiliary_layers"])]
+    out = {}
+    for prefix, L in comps:
+        for k, v in flat.items():
+            if k.startswith(prefix) and "/x_layers/" in k:
+                leaf = k.split("/x_layers/", 1)[1]
+                if v.ndim > 0 and v.shape[0] == L:
+                    for i in range(L):
+                        out[rename(f"{prefix}/layers/{i}/{leaf}")] = v[i]
+    for k, v in flat.items():
+        if "/x_layers/" not in k:
+            out[rename(k)] = v
+    return out
+
+
+def test_load_model_reference_converted_lvt(tmp_path):
+    """A LvT tree renamed and unstacked by convert_weights.py's rules (incl. text_encoder/
+    token_emb/emb_var -> .../weight, mapped back as weight_utils.py:33-34 does) loads through
+    models_mlx.load_model with every leaf bit-identical."""
+    cfg = dict(models.CONFIGS["videoprism_lvt_v1_base"])
+    cfg.update(num_spatial_layers=2, num_temporal_layers=1, num_auxiliary_layers=2,
+               num_unimodal_layers=3, vocabulary_size=50)
+    var = params.synthetic_params(cfg, seed=4, specs=params.clip_leaf_specs(cfg))
+    flat = params.flatten(var["params"])
+    conv = _convert_like_reference(flat, cfg, lvt=True)
+    assert "text_encoder/token_emb/weight" in conv
+    assert len(conv) == sum(v.shape[0] if "/x_layers/" in k else 1 for k, v in flat.items())
+    path = tmp_path / "videoprism_lvt_public_v1_base_mlx.safetensors"
+    from safetensors.numpy import save_file
+    save_file({k: np.ascontiguousarray(v) for k, v in conv.items()}, str(path))
+    clip = models_mlx.load_model("videoprism_lvt_public_v1_base", weights_path=str(path))
+    back = params.canonical_params(clip.variables)
+    specs = params.clip_leaf_specs(cfg)
+    params.validate(back, specs)
+    for k, v in flat.items():
+        np.testing.assert_array_equal(back[k], v)
+
+
+def test_canonical_params_renamed_but_stacked():
+    """Keys renamed to '/weight' while the stacks stay scanned still map back."""
+    cfg = dict(CLIP_TINY)
+    var = params.synthetic_params(cfg, seed=5, specs=params.clip_leaf_specs(cfg))
+    flat = params.flatten(var["params"])
+    ren = {k.replace("/kernel", "/weight").replace("/scale", "/weight").replace("/emb_var", "/weight"): v
+           for k, v in flat.items()}
+    back = params.canonical_params(ren)
+    params.validate(back, params.clip_leaf_specs(cfg))

@@ -60,3 +60,40 @@ def test_gloo_world2_gather_and_timing():
         assert rows == [float(i) for i in range(64)]   # every rank sees all clips in order
         assert t == 2.0                                  # max over ranks
     assert [(lo, hi) for _, lo, hi, _, _ in res] == [(0, 32), (32, 64)]
+
+
+def _bench_standin(workload, batch):
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
+                                                            "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--standin",
+                        "--workload", workload, "--batch", str(batch), "--frames", "2", "--steps", "2",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=150, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    return lines[0]
+
+
+@pytest.mark.timeout(200)
+def test_bench_spawns_world2_base_gather():
+    """`bench.py --gpus 2` without a launcher spawns 2 ranks and drives its real step logic (pool ->
+    gather) with the CPU stand-in forward: rank-major rows of all 2*b clips, n_gpus == 2."""
+    line = _bench_standin("base", 2)
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 4
+    chk = line["standin_check"]
+    assert chk["gathered_shape"] == [4, 768] and chk["row_order_ok"]
+
+
+@pytest.mark.timeout(200)
+def test_bench_spawns_world2_lvt_similarity():
+    """LvT step: video embeddings -> gather -> similarity against the replicated text queries;
+    the similarity covers every clip of both ranks ([2*b, Q], README.md:81)."""
+    line = _bench_standin("lvt_base", 3)
+    assert line["n_gpus"] == 2
+    chk = line["standin_check"]
+    assert chk["gathered_shape"] == [6, 768] and chk["row_order_ok"]
+    assert chk["similarity_shape"] == [6, 8]

@@ -1,0 +1,113 @@
+"""GPU checks of the drop-in boundary's edges: attention without a logit cap or with a cap past
+the max-free softmax's range (layers.py:586-589: cap <= 0 disables capping; FactorizedEncoder's
+default cap is 0.0, encoders.py:407), the host engine's argument validation, the per-class kernel
+symbol the bench's roofline keys its PMC record on, and the C-ABI RCCL all-gather (vp_allgather)
+on a one-rank communicator."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import videoprism_oracle as orc
+from videoprism import distributed, models, params
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(**kw):
+    c = dict(models.CONFIGS["videoprism_v1_base"])
+    c.update(num_spatial_layers=1, num_temporal_layers=1)
+    c.update(kw)
+    return c
+
+
+def _model(cfg, bf16):
+    return models.get_model(None, model_fn=lambda: models.encoders.FactorizedEncoder(**cfg),
+                            fprop_dtype=torch.bfloat16 if bf16 else None)
+
+
+def _pool_l2(e):
+    m = e.astype(np.float64).mean(axis=1)
+    return m / np.sqrt((m * m).sum(-1, keepdims=True) + 1e-12)
+
+
+@pytest.mark.parametrize("cap", [0.0, 120.0])
+def test_uncapped_and_large_cap_attention(cuda, cap):
+    """bf16 with cap 0 (no tanh cap) or 120 (> 80: exp(cap) * S would overflow the max-free fp32
+    softmax) runs the online-softmax kernel; fp32 likewise; both against the fp64 oracle."""
+    cfg = _cfg(atten_logit_cap=cap)
+    var = params.synthetic_params(cfg, seed=8)
+    video = np.random.default_rng(8).random((1, 2, 288, 288, 3), dtype=np.float32)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    emb32, _ = _model(cfg, False).apply(var, video)
+    e32 = np.abs(emb32 - ref).max()
+    emb16, _ = _model(cfg, True).apply(var, video)
+    assert np.isfinite(emb16).all()
+    p16 = np.abs(_pool_l2(emb16) - _pool_l2(ref)).max()
+    print(f"cap {cap}: f32 max-abs {e32:.3e}; bf16 pooled max-abs {p16:.3e}, token mean-abs "
+          f"{np.abs(emb16 - ref).mean():.3e}")
+    assert e32 <= 1e-5
+    assert p16 <= 1e-3
+
+
+def test_engine_rejects_bad_out_and_device(cuda):
+    """Engine.forward hands raw pointers to the C-ABI: a wrong-shaped, strided, wrong-dtype or
+    off-device `out` / `video` is refused before any launch."""
+    cfg = _cfg()
+    var = params.synthetic_params(cfg, seed=1)
+    eng = _model(cfg, True).engine(var, 0)
+    video = torch.rand((1, 2, 288, 288, 3), device=cuda).to(torch.bfloat16)
+    good = torch.empty((1, 512, 768), device=cuda, dtype=torch.bfloat16)
+    eng.forward(video, out=good)
+    for bad in (torch.empty((1, 511, 768), device=cuda, dtype=torch.bfloat16),
+                torch.empty((1, 768, 512), device=cuda, dtype=torch.bfloat16).transpose(1, 2),
+                torch.empty((1, 512, 768), device=cuda, dtype=torch.float16),
+                torch.empty((1, 512, 768), dtype=torch.bfloat16)):
+        with pytest.raises(ValueError):
+            eng.forward(video, out=bad)
+    with pytest.raises(ValueError):
+        eng.forward(video.cpu(), out=good)
+
+
+def test_profile_kernel_symbol(cuda):
+    """vp_profile_kernel_name names the kernel behind each profiled class (the key of the bench's
+    PMC traffic record)."""
+    cfg = _cfg()
+    var = params.synthetic_params(cfg, seed=1)
+    eng = _model(cfg, True).engine(var, 0)
+    video = torch.rand((2, 2, 288, 288, 3), device=cuda).to(torch.bfloat16)
+    eng.profile_enable(64)
+    eng.forward(video)
+    torch.cuda.synchronize()
+    eng.profile_read()
+    eng.profile_enable(0)
+    names = {c: eng.kernel_name(c) for c in ("gemm_ffn1_gelu", "gemm_qkv", "attention_spatial")}
+    print(names)
+    assert names["gemm_ffn1_gelu"].startswith("gemm_bf16_w4_kernel<9")
+    assert names["gemm_qkv"].startswith("gemm_bf16_w4_kernel<8")
+    assert names["attention_spatial"].startswith("attn_spatial_kernel<")
+
+
+def test_rccl_allgather_one_rank(cuda):
+    """The C-ABI collective on real hardware: a one-rank RCCL communicator bootstrapped through
+    torch.distributed (gloo store), vp_allgather of fp32 and bf16 rows."""
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        comm = distributed.Communicator(0)
+        for dt in (torch.float32, torch.bfloat16):
+            x = torch.randn(4, 768, device=cuda).to(dt)
+            y = comm.all_gather_rows(x)
+            torch.cuda.synchronize()
+            assert y.shape == (4, 768) and torch.equal(x, y)
+        comm.close()
+    finally:
+        dist.destroy_process_group()

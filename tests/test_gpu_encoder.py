@@ -2,9 +2,8 @@
 drop-in `models.get_model(...).apply`) against the NumPy oracle.
 
 Tolerances (written here, measured on MI355X):
-  * fprop float32 vs oracle fp64: max-abs <= 5e-5 on LayerNorm-ed O(1) outputs
-    (north_star asks 1e-5 vs JAX fp32; our fp32 and the oracle fp64 differ by fp32
-    accumulation over up to 16 layers; the measured value is printed).
+  * fprop float32 vs oracle fp64: max-abs <= 1e-5 on LayerNorm-ed O(1) outputs (the north_star
+    bar; the measured value is printed).
   * fprop bfloat16 vs oracle fp64: bf16 rounding of every GEMM operand makes per-token
     deviations of a few 1e-2 unavoidable; we bound mean-abs <= 2e-2,
     and max-abs of the L2-normalised mean-pooled clip embedding <= 1e-3 (north_star).
@@ -63,7 +62,7 @@ def test_base_dims_f32(cuda, dist):
     err = np.abs(emb - ref)
     print(f"f32 base-dims max-abs {err.max():.3e} mean-abs {err.mean():.3e}")
     assert emb.shape == (1, 2 * 256, 768)
-    assert err.max() <= 5e-5
+    assert err.max() <= 1e-5
 
 
 def test_base_dims_bf16(cuda):
@@ -92,8 +91,9 @@ def test_frame_paddings_and_intermediate_f32(cuda):
     ref, rout = orc.factorized_encoder(var["params"], video, cfg, mode="f64",
                                        frame_paddings=fp, return_intermediate=True)
     assert set(out) == {"spatial_features"}
-    assert np.abs(emb - ref).max() <= 5e-5
-    assert np.abs(out["spatial_features"] - rout["spatial_features"]).max() <= 5e-5
+    e1, e2 = np.abs(emb - ref).max(), np.abs(out["spatial_features"] - rout["spatial_features"]).max()
+    print(f"f32 padded frames: embeddings max-abs {e1:.3e}, spatial_features {e2:.3e}")
+    assert e1 <= 1e-5 and e2 <= 1e-5
 
 
 def test_frame_paddings_bf16(cuda):
@@ -116,7 +116,9 @@ def test_large_dims_temporal_interpolation_f32(cuda):
     emb, _ = _run(cfg, var, video, bf16=False)
     ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
     assert emb.shape == (1, 16 * 256, 1024)
-    assert np.abs(emb - ref).max() <= 5e-5
+    err = np.abs(emb - ref).max()
+    print(f"f32 large dims T 8->16: max-abs {err:.3e}")
+    assert err <= 1e-5
 
 
 def test_batch_invariance_bitwise_bf16(cuda):
@@ -143,7 +145,7 @@ def test_full_base_b1_f32_vs_oracle(cuda):
     ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f32")
     err = np.abs(emb - ref)
     print(f"full base f32 vs oracle-f32 max-abs {err.max():.3e} mean-abs {err.mean():.3e}")
-    assert err.max() <= 2e-4
+    assert err.max() <= 1e-5
 
 
 def test_full_base_b1_bf16_vs_oracle(cuda):

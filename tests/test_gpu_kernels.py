@@ -147,17 +147,9 @@ def test_gemm_kernels_bitwise_equal(cuda, M, N, K, epi):
         nat.dev_gemm_kernel(which, a, w, b, epi, o, resid=o if resid else None, pos=pos,
                             rowpad=pad if epi != nat.EPI_POS and epi != nat.EPI_POS_BF16 else None)
         outs[which] = o
-    if not f32_out and K >= 704 and M % 256 == 0 and N % 128 == 0:
-        # the overlapped-epilogue kernel: 256x128 tiles, same per-output K order
-        o = x0.to(torch.bfloat16) if resid else torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-        nat.dev_gemm_kernel(2, a, w, b, epi, o, resid=o if resid else None, pos=pos,
-                            rowpad=pad if epi != nat.EPI_POS and epi != nat.EPI_POS_BF16 else None)
-        outs[2] = o
     torch.cuda.synchronize()
     if 4 in outs:
         assert torch.equal(outs[4], outs[8])
-    if 2 in outs and 4 in outs:
-        assert torch.equal(outs[4], outs[2])
     if not outs:
         pytest.skip("shape runs on no kernel under test")
     y = a.double() @ w.double().T + b.double()
@@ -423,21 +415,3 @@ def test_gemm_row_stats(cuda, epi):
     ref = torch.stack([rstd, -mean * rstd], 1)
     assert torch.allclose(rs_p.double(), ref, rtol=2e-5, atol=1e-5)
     assert torch.allclose(rs_r.double(), ref, rtol=2e-5, atol=1e-5)
-
-
-@pytest.mark.parametrize("variant", [16, 32, 48])
-def test_attention_spatial_layout_variants(cuda, variant):
-    """Head-major q|k|v (bit 16) and LDS-staged O stores (bit 32) are bitwise equal to the
-    production spatial kernel on the same values."""
-    nseq, heads, S = 3, 12, 256
-    D = heads * 64
-    qkv = _bf(_qkv(nseq, S, heads, 5)).to(cuda)
-    ref = nat.op_attention(qkv, nseq, S, heads, 50.0)
-    src = qkv
-    if variant & 16:  # [M, 3, heads, 64] -> [3, heads, M, 64]
-        src = qkv.reshape(nseq * S, 3, heads, 64).permute(1, 2, 0, 3).contiguous()
-    out = torch.empty_like(ref)
-    nat.call("vp_dev_attention_diag", variant, src.data_ptr(), out.data_ptr(), nseq, heads, 50.0,
-             torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    assert torch.equal(out, ref)

@@ -4,6 +4,8 @@ attention.hip), interleaved rounds in one process."""
 import os
 import sys
 
+os.environ.setdefault("VP_DIAG_LIB", "1")  # ablation builds live in the diag library
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
 import torch  # noqa: E402

@@ -10,6 +10,8 @@ import ctypes
 import os
 import sys
 
+os.environ.setdefault("VP_DIAG_LIB", "1")  # ablation builds live in the diag library
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
 import torch  # noqa: E402

@@ -46,32 +46,28 @@ for k, cs in vals.items():
         print(f"   => HBM write ~ {m['WRITE_SIZE']*1024/1e6:.1f} MB")
 
 
-# --json OUT: per-launch HBM bytes of the bench's kernel classes (bench.py reads it for the
-# roofline's `traffic`): 2 x FETCH_SIZE (gfx950 rule) + WRITE_SIZE, KiB counters.
-CLASS_OF = {  # kernel instance -> vp_profile class (vp_abi.cpp kProfNames); <EPI, DIAG, PF>
-    "gemm_bf16_w4_kernel<9, 0, 0>": "gemm_ffn1_gelu",      # EPI_GELU_BF16_LN
-    "gemm_bf16_w4_kernel<11, 0, 2>": "gemm_ffn2",          # EPI_RESID_FFN_BF16_ST, A prefetch
-    "gemm_bf16_w4_kernel<8, 0, 0>": "gemm_qkv",            # EPI_BF16_LN
-    "gemm_bf16_w4_kernel<10, 0, 0>": "gemm_post",          # EPI_RESID_BF16_ST
-    "gemm_bf16_w4_kernel<12, 0, 0>": "gemm_patch_embed",   # EPI_POS_BF16_ST
-    "attn_spatial_kernel<false, 0>": "attention_spatial",
-    "attn_temporal_kernel<false>": "attention_temporal",
-}
-if len(sys.argv) > 3 and sys.argv[2] == "--json":
+# --json OUT WORKLOAD: per-launch HBM bytes of every kernel symbol seen in the FETCH_SIZE and
+# WRITE_SIZE passes, keyed by the short symbol (e.g. "gemm_bf16_w4_kernel<9, 512, 0>"), with the
+# source fingerprint of the build that ran (bench.py quotes a record only for the same sources,
+# workload and symbol): 2 x FETCH_SIZE (gfx950 rule) + WRITE_SIZE, KiB counters.
+if len(sys.argv) > 4 and sys.argv[2] == "--json":
     import json
-    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes ({root}); "
-                     "hbm_bytes_per_launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md "
-                     "HBM section: FETCH_SIZE reads half of wide streaming reads on gfx950; Infinity-Cache "
-                     "hits are counted)", "kernels": {}}
+    sys.path[:0] = [os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                 "videoprism-mlx_amd")]
+    from videoprism import _native
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over "
+                     f"`bench.py --workload {sys.argv[4]}` (tools/pmc_traffic.sh); hbm_bytes_per_launch "
+                     "= 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section: FETCH_SIZE "
+                     "reads half of wide streaming reads on gfx950; Infinity-Cache hits are counted)",
+           "workload": sys.argv[4], "src_hash": _native.source_fingerprint(), "kernels": {}}
     for k, cs in vals.items():
-        cls = CLASS_OF.get(k)
-        if not cls or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
         f = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
         w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
-        out["kernels"][cls] = {"kernel": k, "fetch_bytes": 2 * f * 1024, "write_bytes": w * 1024,
-                               "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
-                               "dispatches": len(cs["FETCH_SIZE"])}
+        out["kernels"][k] = {"fetch_bytes": 2 * f * 1024, "write_bytes": w * 1024,
+                             "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+                             "dispatches": len(cs["FETCH_SIZE"])}
     with open(sys.argv[3], "w") as fo:
         json.dump(out, fo, indent=1)
     print("wrote", sys.argv[3])

@@ -456,6 +456,7 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   // O leaves through LDS as whole 128-B row segments (tools/attn_bench.py: 217 -> 209 us at the
   // bench shape); a head-major q|k|v layout measured only 1 % faster and is not used
   const int64_t D = heads * 64;
+  VP_NOTE_KERNEL(fn);
   if (key_pad)
     hipLaunchKernelGGL((attn_spatial_kernel<true, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
                        key_pad, rev, 3 * D, (int64_t)64, D, make_cap_poly(cap));
@@ -465,6 +466,7 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   return hipGetLastError();
 }
 
+#ifdef VP_DIAG
 hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, hipStream_t s) {
   const dim3 grid(num_seq * heads);
@@ -493,12 +495,14 @@ hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int nu
   }
   return hipErrorInvalidValue;
 }
+#endif
 
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s) {
   if (!(cap > 0.0f) || S < 1 || S > 16) return hipErrorInvalidValue;
   const int pairs = num_seq * heads;
   const dim3 grid((pairs + kTpWaves - 1) / kTpWaves);
+  VP_NOTE_KERNEL(key_pad ? (const void*)attn_temporal_kernel<true> : (const void*)attn_temporal_kernel<false>);
   if (key_pad)
     hipLaunchKernelGGL(attn_temporal_kernel<true>, grid, dim3(kTpWaves * 64), 0, s, qkv, o, pairs, S, heads, cap, key_pad);
   else
@@ -518,6 +522,7 @@ hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int hea
     if (e != hipSuccess) return e;
     attr = true;
   }
+  VP_NOTE_KERNEL(attn_f32_kernel);
   hipLaunchKernelGGL(attn_f32_kernel, dim3(num_seq * heads), dim3(256), lds, s, qkv, o, S, heads, cap, key_pad);
   return hipGetLastError();
 }

@@ -310,6 +310,7 @@ hipError_t attention_long_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S,
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const int xcd_map = grid % 8 == 0 ? 1 : 0;
   const CapPoly cp = make_cap_poly(cap);
+  VP_NOTE_KERNEL(attn_long_kernel);
   hipLaunchKernelGGL(attn_long_kernel, dim3((unsigned)grid), dim3(kLgThreads), kLgLds, s, qkv, o, S, heads,
                      nqb, cap, xcd_map, cp);
   return hipGetLastError();
@@ -321,6 +322,7 @@ hipError_t attention_masked(const void* qkv, void* o, int in_is_bf16, int num_se
   const int nqb = (S + kGnQ - 1) / kGnQ;
   const int64_t grid = (int64_t)num_seq * heads * nqb;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  VP_NOTE_KERNEL(in_is_bf16 ? (const void*)attn_masked_kernel<bf16_t> : (const void*)attn_masked_kernel<float>);
   if (in_is_bf16)
     hipLaunchKernelGGL(attn_masked_kernel<bf16_t>, dim3((unsigned)grid), dim3(256), 0, s,
                        (const bf16_t*)qkv, (bf16_t*)o, S, heads, nqb, cap, key_pad, causal);

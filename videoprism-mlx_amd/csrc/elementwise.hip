@@ -5,6 +5,9 @@
 
 namespace vp {
 
+thread_local const void* g_last_kernel = nullptr;
+
+
 namespace {
 
 // ---- patchify (encoders.py:70-104): '(m p)(n q) c -> (m n)(p q c)', K zero-padded ----

@@ -351,6 +351,7 @@ hipError_t launch_one(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus() ? tiles : num_cus();
+  VP_NOTE_KERNEL((gemm_bf16_tn_kernel<EPI, DIAG>));
   hipLaunchKernelGGL((gemm_bf16_tn_kernel<EPI, DIAG>), dim3(grid), dim3(kGemmThreads), kGemmLds, s, A, lda,
                      W, ldw, M, N, K, ep);
   return hipGetLastError();
@@ -367,6 +368,7 @@ const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw) {
   return nullptr;
 }
 
+#ifdef VP_DIAG
 hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
                           int M, int N, int K, const EpiArgs& ep, hipStream_t s) {
   switch (diag) {
@@ -382,6 +384,7 @@ hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* 
   }
   return hipErrorInvalidValue;
 }
+#endif
 
 hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                      int N, int K, const EpiArgs& ep, hipStream_t s) {
@@ -398,25 +401,16 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
   return hipErrorInvalidValue;
 }
 
-// Kernel choice for the forward and vp_op_gemm.  VP_GEMM_KERNEL=w8|w4 forces one kernel
-// (A/B runs of tools/ and bench.py); default: the 4-wave kernel wherever its 32-bit buffer
-// offsets reach, except the shapes where the 8-wave kernel measured faster.
+// Kernel choice for the forward and vp_op_gemm: the 4-wave kernel wherever its 32-bit buffer
+// offsets reach (the forward chunks its batch so that they always do), except the fp32-residual
+// epilogues at K < 1024 (text tower), where the 8-wave kernel measured faster.
 hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                           int N, int K, const EpiArgs& ep, hipStream_t s) {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("VP_GEMM_KERNEL");
-    mode = (e && !strcmp(e, "w8")) ? 8 : (e && !strcmp(e, "w4")) ? 4 : (e && !strcmp(e, "ov")) ? 2 : 0;
-  }
-  if (mode == 2 && gemm_bf16_ov_ok(epi, M, N, K, lda, ldw))
-    return gemm_bf16_ov(epi, A, lda, W, ldw, M, N, K, ep, s);
   const bool w4_ok = (uint64_t)M * (uint64_t)lda * 2 < 0xFFFFFFF0ull &&
                      (uint64_t)N * (uint64_t)ldw * 2 < 0xFFFFFFF0ull;
-  bool use_w4 = w4_ok;
   if (epi >= EPI_BF16_LN) return w4_ok ? gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s) : hipErrorInvalidValue;
-  if (mode == 8) use_w4 = false;
-  else if (mode != 4 && (epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024) use_w4 = false;
-  if (use_w4) return gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s);
+  if (w4_ok && !((epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024))
+    return gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s);
   return gemm_bf16(epi, A, lda, W, ldw, M, N, K, ep, s);
 }
 

@@ -432,6 +432,7 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
+  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF>));
   hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
                      ldw, M, N, K, ep);
   return hipGetLastError();
@@ -485,7 +486,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
   if ((uint64_t)M * (uint64_t)lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * (uint64_t)ldw * 2 >= 0xFFFFFFF0ull)
     return hipErrorInvalidValue;
   if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
-  if (epi >= 1000) {  // ablation builds, EPI_BF16 epilogue
+#ifdef VP_DIAG
+  if (epi >= 1000) {  // ablation builds (tools' diag library only), EPI_BF16 epilogue
     switch (epi - 1000) {
       case 2: return launch_w4<EPI_BF16, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 4: return launch_w4<EPI_BF16, 4>(A, lda, W, ldw, M, N, K, ep, s);
@@ -510,13 +512,13 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
     }
     return hipErrorInvalidValue;
   }
+#endif
   // nontemporal output stores: +1.7 % on the whole forward vs plain stores (same device,
   // back-to-back runs: 947.8 vs 931.7 clips/s)
   // (also measured, no difference in the full forward: plain stores on the residual-stream
   // producers so x stays in the Infinity Cache, and the A prefetch on the LayerNorm-folded
   // consumers: 912-915 clips/s for all four combinations on one device)
   return w4_dispatch<0>(epi, A, lda, W, ldw, M, N, K, ep, s);
-  return hipErrorInvalidValue;
 }
 
 }  // namespace vp

@@ -129,6 +129,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 template <int EPI>
 hipError_t launch(const float* A, int64_t lda, const float* W, int64_t ldw, int M, int N, int K,
                   const EpiArgs& ep, hipStream_t s) {
+  VP_NOTE_KERNEL(gemm_f32_kernel<EPI>);
   hipLaunchKernelGGL(gemm_f32_kernel<EPI>, dim3((M / TM) * (N / TN)), dim3(256), 0, s, A, lda, W,
                      ldw, M, N, K, ep);
   return hipGetLastError();

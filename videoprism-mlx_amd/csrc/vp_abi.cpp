@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
+#include <cxxabi.h>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -38,6 +40,7 @@ int vp_create(const vp_config* cfg, int device, vp_handle** out) {
     return fail(VP_EINVAL, "bad patch_size / pos_emb_shape");
   if (cfg->num_spatial_layers < 0 || cfg->num_temporal_layers < 0)
     return fail(VP_EINVAL, "negative layer count");
+  if (!std::isfinite(cfg->atten_logit_cap)) return fail(VP_EINVAL, "atten_logit_cap must be finite");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return fail(VP_EINVAL, "invalid HIP device " + std::to_string(device));
@@ -204,23 +207,23 @@ int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int6
   if (!h || !bytes) return fail(VP_EINVAL, "null argument");
   int rc = check_geometry(h, B, T, H, W);
   if (rc) return rc;
-  *bytes = ws_layout(h, B, T, H, W).total;
+  *bytes = ws_layout(h, chunk_of(h, B, T, H, W), T, H, W).total;
   return VP_OK;
 }
 
-int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
-               int64_t W, const float* frame_paddings, void* out, int out_dtype,
-               void* spatial_out, void* workspace, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// FactorizedEncoder.__call__ over one chunk of B clips (B <= chunk_clips, so every GEMM operand
+// fits the 32-bit buffer range); vp_forward below walks the batch chunk by chunk
+int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
+                  int64_t W, const float* frame_paddings, void* out, int out_dtype,
+                  void* spatial_out, void* workspace, void* stream) {
   using namespace vp;
-  if (!h || !video || !out || !workspace) return fail(VP_EINVAL, "null argument");
-  if (!h->finalized) return fail(VP_ESTATE, "vp_finalize has not been called");
-  if ((in_dtype != VP_F32 && in_dtype != VP_BF16 && in_dtype != VP_U8) ||
-      (out_dtype != VP_F32 && out_dtype != VP_BF16))
-    return fail(VP_EINVAL, "bad dtype");
-  int rc = check_geometry(h, B, T, H, W);
-  if (rc) return rc;
+  int rc;
   const WsLayout L = ws_layout(h, B, T, H, W);
-  if (ws_bytes < L.total) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(L.total));
+
   VP_HIP(hipSetDevice(h->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const vp_config& c = h->cfg;
@@ -309,6 +312,38 @@ int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t
   return VP_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int vp_forward(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
+               int64_t W, const float* frame_paddings, void* out, int out_dtype,
+               void* spatial_out, void* workspace, size_t ws_bytes, void* stream) {
+  if (!h || !video || !out || !workspace) return fail(VP_EINVAL, "null argument");
+  if (!h->finalized) return fail(VP_ESTATE, "vp_finalize has not been called");
+  if ((in_dtype != VP_F32 && in_dtype != VP_BF16 && in_dtype != VP_U8) ||
+      (out_dtype != VP_F32 && out_dtype != VP_BF16))
+    return fail(VP_EINVAL, "bad dtype");
+  int rc = check_geometry(h, B, T, H, W);
+  if (rc) return rc;
+  const int64_t Bc = chunk_of(h, B, T, H, W);
+  const size_t need = ws_layout(h, Bc, T, H, W).total;
+  if (ws_bytes < need) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(need));
+  // per-clip strides of the caller's buffers
+  const int64_t P = h->cfg.patch_size, D = h->cfg.model_dim;
+  const size_t in_clip = (size_t)(T * H * W * 3) * (in_dtype == VP_U8 ? 1 : in_dtype == VP_BF16 ? 2 : 4);
+  const size_t out_clip = (size_t)(T * (H / P) * (W / P) * D) * (out_dtype == VP_BF16 ? 2 : 4);
+  for (int64_t b0 = 0; b0 < B; b0 += Bc) {
+    const int64_t nb = std::min(Bc, B - b0);
+    rc = forward_chunk(h, static_cast<const char*>(video) + b0 * in_clip, in_dtype, nb, T, H, W,
+                       frame_paddings ? frame_paddings + b0 * T : nullptr, static_cast<char*>(out) + b0 * out_clip,
+                       out_dtype, spatial_out ? static_cast<char*>(spatial_out) + b0 * out_clip : nullptr,
+                       workspace, stream);
+    if (rc) return rc;
+  }
+  return VP_OK;
+}
+
 // ----------------------------------- profiling ----------------------------------------
 
 int vp_profile_enable(vp_handle* h, int capacity) {
@@ -361,6 +396,23 @@ int vp_profile_class_name(int cls, const char** name) {
 
 int vp_profile_class_count(void) { return PC_COUNT; }
 
+int vp_profile_kernel_name(vp_handle* h, int cls, const char** name) {
+  if (!h || cls < 0 || cls >= PC_COUNT || !name) return fail(VP_EINVAL, "bad argument");
+  Profiler& p = h->prof;
+  p.kname[cls].clear();
+  if (p.kfn[cls]) {
+    const char* raw = hipKernelNameRefByPtr(p.kfn[cls], nullptr);
+    if (raw) {
+      int st = 0;
+      char* dm = abi::__cxa_demangle(raw, nullptr, nullptr, &st);
+      p.kname[cls] = (st == 0 && dm) ? dm : raw;
+      std::free(dm);
+    }
+  }
+  *name = p.kname[cls].c_str();
+  return VP_OK;
+}
+
 // ----------------------------------- op level -----------------------------------------
 
 int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const void* W, int64_t ldw,
@@ -394,6 +446,7 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
   return VP_OK;
 }
 
+#ifdef VP_DIAG
 // Not in the public header: ablation builds of the bf16 GEMM (tools/gemm_bench.py).
 int vp_dev_gemm_diag(int diag, const void* A, const void* W, int64_t M, int64_t N, int64_t K,
                      void* out, const float* bias, void* stream) {
@@ -406,9 +459,10 @@ int vp_dev_gemm_diag(int diag, const void* A, const void* W, int64_t M, int64_t 
                         static_cast<hipStream_t>(stream)));
   return VP_OK;
 }
+#endif
 
-// Not in the public header: one named bf16 GEMM kernel (which = 2: gemm_bf16_ov, 4: gemm_bf16_w4,
-// 8: gemm_bf16)
+// Not in the public header: one named bf16 GEMM kernel (4: gemm_bf16_w4, 8: gemm_bf16; the tools'
+// diag library adds 2: gemm_bf16_ov)
 // with any epilogue, for kernel A/B tests (tests/test_gpu_kernels.py) and tools/gemm_bench.py.
 // epi >= 1000 selects the 4-wave kernel's ablation builds.
 int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t M, int64_t N,
@@ -427,12 +481,15 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
     VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
   else if (which == 8)
     VP_HIP(gemm_bf16(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
+#ifdef VP_DIAG
   else if (which == 2) {
     if (!gemm_bf16_ov_ok(epi >= 1000 ? 0 : epi, (int)M, (int)N, (int)K, K, K))
       return fail(VP_EINVAL, "shape/epilogue not supported by gemm_bf16_ov");
     VP_HIP(gemm_bf16_ov(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
-  } else
-    return fail(VP_EINVAL, "which must be 2, 4 or 8");
+  }
+#endif
+  else
+    return fail(VP_EINVAL, "which must be 4 or 8 (2: diag library)");
   return VP_OK;
 }
 
@@ -457,6 +514,7 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
   return VP_OK;
 }
 
+#ifdef VP_DIAG
 // ablation builds of the spatial attention kernel (tools/attn_bench.py)
 int vp_dev_attention_diag(int diag, const void* qkv, void* o, int64_t num_seq, int64_t heads, float cap,
                           void* stream) {
@@ -464,6 +522,7 @@ int vp_dev_attention_diag(int diag, const void* qkv, void* o, int64_t num_seq, i
                                     static_cast<hipStream_t>(stream)));
   return VP_OK;
 }
+#endif
 
 // which = 0: ln_stats_finalize(src = st_part [D/128][M][2]); 1: ln_row_stats(src = bf16 [M][D])
 int vp_dev_ln_stats(int which, const void* src, int64_t M, int64_t D, float* ln_rs, void* stream) {
@@ -481,7 +540,9 @@ int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, in
   if (!qkv || !o || num_seq < 1 || heads < 1) return fail(VP_EINVAL, "bad argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (precision == VP_BF16) {
-    if (!(cap > 0.0f)) return fail(VP_ENOTSUP, "bf16 attention requires atten_logit_cap > 0");
+    if (!fast_cap(cap))
+      return fail(VP_ENOTSUP, "bf16 vp_op_attention requires 0 < cap <= 80 (max-free softmax); "
+                              "use vp_op_attention_masked for other caps");
     if (S == 256)
       VP_HIP(attention_spatial_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)heads, cap, key_pad, s));
     else if (S > 256 && S % 256 == 0 && !key_pad)

@@ -339,26 +339,26 @@ int vp_clip_video_workspace_bytes(const vp_clip* c, int64_t B, int64_t T, int64_
   size_t inner = 0;
   int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
   if (rc) return rc;
-  *bytes = clip_video_ws(c, B, T, H, W, inner).total;
+  *bytes = clip_video_ws(c, chunk_of(c->video, B, T, H, W), T, H, W, inner).total;
   return VP_OK;
 }
 
-int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H, int64_t W,
-                         const float* frame_paddings, int normalize, float* video_emb, float* frame_emb,
-                         void* spatial_out, void* spatiotemporal_out, int out_dtype, void* workspace,
-                         size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// video side of FactorizedVideoCLIP over one chunk of B <= chunk_clips clips
+int clip_video_chunk(vp_clip* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H, int64_t W,
+                     const float* frame_paddings, int normalize, float* video_emb, float* frame_emb,
+                     void* spatial_out, void* spatiotemporal_out, void* workspace, void* stream) {
   using namespace vp;
-  if (!c || !video || !video_emb || !workspace) return fail(VP_EINVAL, "null argument");
-  if (!c->finalized) return fail(VP_ESTATE, "vp_clip_finalize has not been called");
   const bool bf = c->bf16();
   const int fdt = bf ? VP_BF16 : VP_F32;
-  if (spatiotemporal_out && out_dtype != fdt)
-    return fail(VP_EINVAL, "spatiotemporal_features are returned in the fprop dtype");
   size_t inner = 0;
   int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
   if (rc) return rc;
   const ClipVideoWs L = clip_video_ws(c, B, T, H, W, inner);
-  if (ws_bytes < L.total) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(L.total));
+
   const vp_config& v = c->cfg.video;
   const int P = v.patch_size, N = (int)((H / P) * (W / P)), D = v.model_dim, NH = v.num_heads;
   const int S = (int)T * N;
@@ -410,6 +410,46 @@ int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B,
   };
   if ((rc = pool((int)B, S, video_emb))) return rc;
   if (frame_emb && (rc = pool((int)(B * T), N, frame_emb))) return rc;
+  return VP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H, int64_t W,
+                         const float* frame_paddings, int normalize, float* video_emb, float* frame_emb,
+                         void* spatial_out, void* spatiotemporal_out, int out_dtype, void* workspace,
+                         size_t ws_bytes, void* stream) {
+  if (!c || !video || !video_emb || !workspace) return fail(VP_EINVAL, "null argument");
+  if (!c->finalized) return fail(VP_ESTATE, "vp_clip_finalize has not been called");
+  const int fdt = c->bf16() ? VP_BF16 : VP_F32;
+  if (spatiotemporal_out && out_dtype != fdt)
+    return fail(VP_EINVAL, "spatiotemporal_features are returned in the fprop dtype");
+  if ((in_dtype != VP_F32 && in_dtype != VP_BF16 && in_dtype != VP_U8) ||
+      (out_dtype != VP_F32 && out_dtype != VP_BF16))
+    return fail(VP_EINVAL, "bad dtype");
+  size_t need = 0;
+  int rc = vp_clip_video_workspace_bytes(c, B, T, H, W, &need);
+  if (rc) return rc;
+  if (ws_bytes < need) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(need));
+  // the batch in chunks of independent clips (each chunk's GEMM operands within 4 GiB)
+  const int64_t Bc = chunk_of(c->video, B, T, H, W);
+  const vp_config& v = c->cfg.video;
+  const int64_t N = (H / v.patch_size) * (W / v.patch_size), D = v.model_dim;
+  const size_t in_clip = (size_t)(T * H * W * 3) * (in_dtype == VP_U8 ? 1 : in_dtype == VP_BF16 ? 2 : 4);
+  // spatial and spatio-temporal features are written in the fprop dtype (vp_forward's out dtype)
+  const size_t st_clip = (size_t)(T * N * D) * (c->bf16() ? 2 : 4);
+  for (int64_t b0 = 0; b0 < B; b0 += Bc) {
+    const int64_t nb = std::min(Bc, B - b0);
+    rc = clip_video_chunk(c, static_cast<const char*>(video) + b0 * in_clip, in_dtype, nb, T, H, W,
+                          frame_paddings ? frame_paddings + b0 * T : nullptr, normalize, video_emb + b0 * D,
+                          frame_emb ? frame_emb + b0 * T * D : nullptr,
+                          spatial_out ? static_cast<char*>(spatial_out) + b0 * st_clip : nullptr,
+                          spatiotemporal_out ? static_cast<char*>(spatiotemporal_out) + b0 * st_clip : nullptr,
+                          workspace, stream);
+    if (rc) return rc;
+  }
   return VP_OK;
 }
 
@@ -583,30 +623,29 @@ int vp_classifier_workspace_bytes(const vp_classifier* c, int64_t B, int64_t T, 
   size_t inner = 0;
   int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
   if (rc) return rc;
-  const ClipVideoWs L = pool_video_ws(c->cfg, B, T, H, W, inner, c->cfg.model_dim / c->cfg.num_heads);
-  *bytes = L.total + align256((size_t)B * c->cfg.model_dim * 4);
+  const int64_t Bc = chunk_of(c->video, B, T, H, W);
+  const ClipVideoWs L = pool_video_ws(c->cfg, Bc, T, H, W, inner, c->cfg.model_dim / c->cfg.num_heads);
+  *bytes = L.total + align256((size_t)Bc * c->cfg.model_dim * 4);
   return VP_OK;
 }
 
-int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
-                          int64_t W, const float* frame_paddings, float* logits, float* embeddings,
-                          void* spatial_out, void* spatiotemporal_out, int out_dtype, void* workspace,
-                          size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// FactorizedVideoClassifier over one chunk of B <= chunk_clips clips
+int classifier_chunk(vp_classifier* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
+                     int64_t W, const float* frame_paddings, float* logits, float* embeddings,
+                     void* spatial_out, void* spatiotemporal_out, void* workspace, void* stream) {
   using namespace vp;
-  if (!c || !video || !logits || !workspace) return fail(VP_EINVAL, "null argument");
-  if (!c->finalized) return fail(VP_ESTATE, "vp_classifier_finalize has not been called");
   const bool bf = c->bf16();
   const int fdt = bf ? VP_BF16 : VP_F32;
-  if (spatiotemporal_out && out_dtype != fdt)
-    return fail(VP_EINVAL, "spatiotemporal_features are returned in the fprop dtype");
-  size_t inner = 0, need = 0;
+  size_t inner = 0;
   int rc = vp_workspace_bytes(c->video, B, T, H, W, &inner);
   if (rc) return rc;
   const vp_config& v = c->cfg;
   const int D = v.model_dim, NH = v.num_heads;
   const ClipVideoWs L = pool_video_ws(v, B, T, H, W, inner, D / NH);
-  if ((rc = vp_classifier_workspace_bytes(c, B, T, H, W, &need))) return rc;
-  if (ws_bytes < need) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(need));
   const int P = v.patch_size, N = (int)((H / P) * (W / P));
   const int M = (int)(B * T * N);
   char* ws = static_cast<char*>(workspace);
@@ -629,6 +668,43 @@ int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int
                        reinterpret_cast<float*>(ws + L.enc), reinterpret_cast<float*>(ws + L.pooled)};
   if ((rc = run_pooler(f, c->pool, feat, M, (int)B, (int)(T * N), D, NH, sc, 0, emb))) return rc;
   VP_HIP(small_gemm(emb, D, 0, c->wproj, 0, c->bproj, 0, logits, c->num_classes, 0, (int)B, c->num_classes, D, 1, s));
+  return VP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
+                          int64_t W, const float* frame_paddings, float* logits, float* embeddings,
+                          void* spatial_out, void* spatiotemporal_out, int out_dtype, void* workspace,
+                          size_t ws_bytes, void* stream) {
+  if (!c || !video || !logits || !workspace) return fail(VP_EINVAL, "null argument");
+  if (!c->finalized) return fail(VP_ESTATE, "vp_classifier_finalize has not been called");
+  const int fdt = c->bf16() ? VP_BF16 : VP_F32;
+  if (spatiotemporal_out && out_dtype != fdt)
+    return fail(VP_EINVAL, "spatiotemporal_features are returned in the fprop dtype");
+  if ((in_dtype != VP_F32 && in_dtype != VP_BF16 && in_dtype != VP_U8) ||
+      (out_dtype != VP_F32 && out_dtype != VP_BF16))
+    return fail(VP_EINVAL, "bad dtype");
+  size_t need = 0;
+  int rc = vp_classifier_workspace_bytes(c, B, T, H, W, &need);
+  if (rc) return rc;
+  if (ws_bytes < need) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(need));
+  const int64_t Bc = chunk_of(c->video, B, T, H, W);
+  const int64_t N = (H / c->cfg.patch_size) * (W / c->cfg.patch_size), D = c->cfg.model_dim;
+  const size_t in_clip = (size_t)(T * H * W * 3) * (in_dtype == VP_U8 ? 1 : in_dtype == VP_BF16 ? 2 : 4);
+  const size_t st_clip = (size_t)(T * N * D) * (c->bf16() ? 2 : 4);  // features in the fprop dtype
+  for (int64_t b0 = 0; b0 < B; b0 += Bc) {
+    const int64_t nb = std::min(Bc, B - b0);
+    rc = classifier_chunk(c, static_cast<const char*>(video) + b0 * in_clip, in_dtype, nb, T, H, W,
+                          frame_paddings ? frame_paddings + b0 * T : nullptr, logits + b0 * c->num_classes,
+                          embeddings ? embeddings + b0 * D : nullptr,
+                          spatial_out ? static_cast<char*>(spatial_out) + b0 * st_clip : nullptr,
+                          spatiotemporal_out ? static_cast<char*>(spatiotemporal_out) + b0 * st_clip : nullptr,
+                          workspace, stream);
+    if (rc) return rc;
+  }
   return VP_OK;
 }
 

@@ -105,6 +105,8 @@ inline const char* kProfNames[PC_COUNT] = {"patchify", "gemm_patch_embed", "laye
 
 // HIP-event profiler: start/stop events around each launch on the launch stream.
 struct Profiler {
+  const void* kfn[PC_COUNT] = {};  // host function of the last kernel launched per class
+  std::string kname[PC_COUNT];    // its demangled name (vp_profile_kernel_name)
   int cap = 0, used = 0;
   uint32_t mask = 0xffffffffu;  // kernel classes that get events (vp_profile_set_mask)
   std::vector<hipEvent_t> ev;
@@ -369,6 +371,20 @@ inline WsLayout ws_layout(const vp_handle* h, int64_t B, int64_t T, int64_t H, i
   return L;
 }
 
+// Clips per forward chunk.  The bf16 GEMM stages its A operand through a buffer descriptor with
+// 32-bit byte offsets, so every GEMM's padded rows x lda x 2 B must stay below 4 GiB (the widest A
+// is the FFN hidden activation, lda = mlp_dim).  The forward entry points process any B as
+// consecutive chunks of at most this many clips (clips are independent, encoders.py:411-580), each
+// in the same workspace.  0: a single clip is already too large.
+inline int64_t chunk_clips(const vp_config& c, int64_t T, int64_t H, int64_t W) {
+  const int64_t P = c.patch_size;
+  const int64_t tok = T * (H / P) * (W / P);
+  const int64_t kpad = ((P * P * 3 + 63) / 64) * 64;
+  const int64_t lda = std::max<int64_t>(std::max<int64_t>(c.model_dim, c.mlp_dim), kpad);
+  const int64_t max_rows = (int64_t)(0xFFFFFFF0ull / (uint64_t)(2 * lda)) / 256 * 256;
+  return tok > 0 ? max_rows / tok : 0;
+}
+
 inline int check_geometry(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W) {
   const int64_t P = h->cfg.patch_size;
   if (B < 1 || T < 1 || H < 1 || W < 1) return fail(VP_EINVAL, "inputs must be [B, T, H, W, 3] with positive sizes");
@@ -377,13 +393,26 @@ inline int check_geometry(const vp_handle* h, int64_t B, int64_t T, int64_t H, i
     return fail(VP_EINVAL, "Image height (" + std::to_string(H) + ") and width (" + std::to_string(W) +
                                ") should be multiples of patch_size (" + std::to_string(P) + ").");
   if (T > kMaxT) return fail(VP_ENOTSUP, "T > 32 frames not supported");
-  if (B * T * (H / P) * (W / P) > 0x7f000000) return fail(VP_ENOTSUP, "too many tokens");
+  if (chunk_clips(h->cfg, T, H, W) < 1)
+    return fail(VP_ENOTSUP, "one clip of " + std::to_string(T) + "x" + std::to_string(H) + "x" + std::to_string(W) +
+                                " exceeds the GEMM operand range (4 GiB per operand)");
   return VP_OK;
+}
+
+// clips per chunk for a forward over B clips
+inline int64_t chunk_of(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W) {
+  return std::min<int64_t>(B, chunk_clips(h->cfg, T, H, W));
 }
 
 }  // namespace
 
 namespace vpi {
+
+// The bf16 attention kernels compute the capped softmax without a running max: every numerator
+// is exp(l) with |l| <= cap, so the fp32 row sum over S <= 4096 keys stays finite (and exact to
+// rounding) while cap <= 80 (e^80 * 4096 < FLT_MAX).  Other caps take the online-softmax kernel.
+constexpr float kMaxFastCap = 80.0f;
+inline bool fast_cap(float cap) { return cap > 0.0f && cap <= kMaxFastCap; }
 
 // which attention kernel a stack uses (the rest of the pre-LN layer is shared)
 enum AttnKind {
@@ -409,11 +438,17 @@ struct Fwd {
   // profiled launch: records events around `fn` when vp_profile_enable() is active
   template <class Fn>
   hipError_t rec(int cls, double flops, double bytes, Fn&& fn) {
-    if (!pf || pf->used >= pf->cap || !((pf->mask >> cls) & 1u)) return fn();
+    auto launch = [&]() {
+      vp::g_last_kernel = nullptr;
+      const hipError_t e = fn();
+      if (pf && vp::g_last_kernel) pf->kfn[cls] = vp::g_last_kernel;
+      return e;
+    };
+    if (!pf || pf->used >= pf->cap || !((pf->mask >> cls) & 1u)) return launch();
     const int i = pf->used++;
     hipError_t e = hipEventRecord(pf->ev[2 * i], s);
     if (e != hipSuccess) return e;
-    e = fn();
+    e = launch();
     if (e != hipSuccess) return e;
     pf->cls[i] = cls; pf->flops[i] = flops; pf->bytes[i] = bytes;
     return hipEventRecord(pf->ev[2 * i + 1], s);
@@ -467,6 +502,9 @@ struct Fwd {
       }
       VP_HIP(rec(acls, aflops, abytes, [&] {
         if (kind == ATT_TEXT) return attention_masked(big, hb, bf, num_seq, S, NH, cap, pad, causal, s);
+        // the bf16 kernels' max-free softmax needs 0 < cap <= kMaxFastCap; cap <= 0 (no capping,
+        // layers.py:586-589) or a larger cap runs the online-softmax kernel
+        if (bf && !fast_cap(cap)) return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s);
         if (kind == ATT_LONG) {
           if (bf) return attention_long_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, s);
           return attention_masked(big, hb, 0, num_seq, S, NH, cap, nullptr, 0, s);

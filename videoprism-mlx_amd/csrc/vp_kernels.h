@@ -8,6 +8,12 @@ namespace vp {
 
 typedef uint16_t bf16_t;
 
+// host function of the kernel most recently launched by this thread through the launchers below
+// (vp_profile_kernel_name names the kernel behind each profiled class, so bench.py can match the
+// PMC traffic of exactly that kernel symbol)
+extern thread_local const void* g_last_kernel;
+#define VP_NOTE_KERNEL(fn) (::vp::g_last_kernel = reinterpret_cast<const void*>(fn))
+
 enum Epilogue {
   EPI_BF16 = 0,       // out_bf16 = acc + bias                       (fused q|k|v projection)
   EPI_GELU_BF16 = 1,  // out_bf16 = gelu(acc + bias) * (1 - rowpad)  (ffn_layer1)
@@ -58,16 +64,16 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 // staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
-// 4-wave, 256x128 tile, two accumulator sets: the epilogue of tile j runs under the MFMAs of
+// [diag library only] 4-wave, 256x128 tile, two accumulator sets: the epilogue of tile j runs under the MFMAs of
 // tile j+1 (gemm_bf16_ov.hip).  bf16-output epilogues, M % 256, N % 128, K % 64, K >= 704.
 bool gemm_bf16_ov_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw);
 hipError_t gemm_bf16_ov(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
-// picks gemm_bf16_w4 or gemm_bf16 by shape (VP_GEMM_KERNEL=ov|w4|w8 overrides)
+// picks gemm_bf16_w4 or gemm_bf16 by epilogue and shape
 hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                           int N, int K, const EpiArgs& ep, hipStream_t s);
 
-// ablation builds of the bf16 GEMM (store epilogue) for tools/gemm_bench.py
+// [diag library only] ablation builds of the bf16 GEMM (store epilogue) for tools/gemm_bench.py
 hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
                           int M, int N, int K, const EpiArgs& ep, hipStream_t s);
 
@@ -81,7 +87,7 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
 // o: rows of D = heads*64.  key_pad: optional [num_seq * S] (1 = padded key).
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, const float* key_pad, hipStream_t s);
-// ablation builds of the spatial kernel (tools/attn_bench.py)
+// [diag library only] ablation builds of the spatial kernel (tools/attn_bench.py)
 hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, hipStream_t s);
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,

@@ -13,8 +13,11 @@ from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t
 
 _LIB_NAME = "libvideoprism_hip.so"
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
+# tools' A/B library (`make -C videoprism-mlx_amd diag`): the product library plus ablation builds;
+# loaded only when VP_DIAG_LIB=1 (tools/), never by the package's tests or the bench
+_DIAG_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvideoprism_hip_diag.so")
 
-VP_OK, VP_EINVAL, VP_ENOMEM, VP_EHIP, VP_ESTATE, VP_ENOTSUP = range(6)
+VP_OK, VP_EINVAL, VP_ENOMEM, VP_EHIP, VP_ESTATE, VP_ENOTSUP, VP_ECOMM = range(7)
 VP_F32, VP_BF16, VP_U8 = 0, 1, 2
 
 EPI_STORE, EPI_GELU, EPI_RESID, EPI_POS, EPI_RESID_FFN = 0, 1, 2, 3, 4
@@ -79,6 +82,13 @@ _SIGNATURES = {
     "vp_profile_set_mask": (c_int, [c_void_p, ctypes.c_uint32]),
     "vp_profile_class_count": (c_int, []),
     "vp_profile_class_name": (c_int, [c_int, POINTER(c_char_p)]),
+    "vp_profile_kernel_name": (c_int, [c_void_p, c_int, POINTER(c_char_p)]),
+    # multi-GPU: RCCL all-gather of pooled clip embeddings
+    "vp_comm_id_bytes": (c_int, []),
+    "vp_comm_unique_id": (c_int, [c_void_p, c_int64]),
+    "vp_comm_init": (c_int, [c_void_p, c_int64, c_int, c_int, c_int, POINTER(c_void_p)]),
+    "vp_comm_destroy": (c_int, [c_void_p]),
+    "vp_allgather": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "vp_op_gemm": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64,
                            c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
                            c_int64, c_void_p, c_void_p]),
@@ -129,14 +139,23 @@ _SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+}
+# diag library only (ablation builds for tools/)
+_DIAG_SIGNATURES = {
     "vp_dev_attention_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
+    "vp_dev_gemm_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
+                                 c_void_p, c_void_p]),
 }
 
 _lib = None
 
 
+def _diag() -> bool:
+    return os.environ.get("VP_DIAG_LIB", "0") == "1"
+
+
 def library_path() -> str:
-    return _LIB_PATH
+    return _DIAG_LIB_PATH if _diag() else _LIB_PATH
 
 
 def load() -> ctypes.CDLL:
@@ -144,15 +163,21 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(_LIB_PATH):
+    path = library_path()
+    if not os.path.exists(path):
         raise NativeLibraryError(
-            f"{_LIB_PATH} not found: build it with `make -C videoprism-mlx_amd` "
+            f"{path} not found: build it with `make -C videoprism-mlx_amd` "
             "(or __graft_entry__.build()); there is no CPU fallback.")
     try:
-        lib = ctypes.CDLL(_LIB_PATH)
+        import torch  # noqa: F401  (HIP runtime / RCCL of the process: torch's, loaded first)
+    except ImportError:  # pragma: no cover
+        pass
+    try:
+        lib = ctypes.CDLL(path)
     except OSError as e:
-        raise NativeLibraryError(f"failed to load {_LIB_PATH}: {e}") from e
-    for name, (res, args) in _SIGNATURES.items():
+        raise NativeLibraryError(f"failed to load {path}: {e}") from e
+    sigs = dict(_SIGNATURES, **(_DIAG_SIGNATURES if _diag() else {}))
+    for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -311,3 +336,45 @@ def op_pool_l2(emb, stream=None):
     out = torch.empty((B, D), dtype=torch.float32, device=emb.device)
     call("vp_op_pool_l2", _ptr(emb), _prec(emb), B, L, D, _ptr(out), _stream(stream))
     return out
+
+
+def source_fingerprint() -> str:
+    """sha256 over the library's sources (csrc/ and include/): bench.py only quotes PMC traffic
+    measured on a build of exactly these sources."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = []
+    for d in (os.path.join(root, "csrc"), os.path.join(os.path.dirname(root), "include")):
+        if os.path.isdir(d):
+            files += sorted(os.path.join(d, f) for f in os.listdir(d)
+                            if f.endswith((".hip", ".cpp", ".h")))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def kernel_short_name(symbol: str) -> str:
+    """'void vp::(anonymous namespace)::gemm_bf16_w4_kernel<9, 512, 0>(...)' ->
+    'gemm_bf16_w4_kernel<9, 512, 0>' (the same key tools/pmc_summary.py gives rocprof's names)."""
+    import re
+    m = re.search(r"(\w+_kernel)<([^>]*)>", symbol)
+    if m:
+        return f"{m.group(1)}<{m.group(2)}>"
+    m = re.search(r"(\w+_kernel)\b", symbol)
+    return m.group(1) if m else symbol
+
+
+def profile_kernel_name(handle, cls_name: str) -> str:
+    """Short symbol of the kernel last launched for profiler class `cls_name` on `handle`."""
+    lib = load()
+    for i in range(lib.vp_profile_class_count()):
+        n = ctypes.c_char_p()
+        call("vp_profile_class_name", i, ctypes.byref(n))
+        if n.value.decode() == cls_name:
+            k = ctypes.c_char_p()
+            call("vp_profile_kernel_name", handle, i, ctypes.byref(k))
+            return kernel_short_name(k.value.decode()) if k.value else ""
+    return ""

@@ -37,6 +37,12 @@ def _is_bf16_dtype(dt) -> bool:
     return "bfloat16" in str(name) or "bfloat16" in str(dt)
 
 
+def _check_device(t, device: int, what: str) -> None:
+    """Tensors handed to the C-ABI must live on the handle's device (raw pointers + its stream)."""
+    if not t.is_cuda or t.device.index != device:
+        raise ValueError(f"{what} must be on cuda:{device} (the engine's device), got {t.device}")
+
+
 def _profile_enable(handle, capacity: int) -> None:
     _native.call("vp_profile_enable", handle, int(capacity))
 
@@ -121,6 +127,10 @@ class Engine:
     def profile_only(self, names=None) -> None:
         _profile_set_mask(self._h, names)
 
+    def kernel_name(self, cls_name: str) -> str:
+        """Short symbol of the kernel behind profiler class `cls_name` (last launch)."""
+        return _native.profile_kernel_name(self._h, cls_name)
+
     def workspace(self, B, T, H, W):
         torch = _torch()
         n = ctypes.c_size_t()
@@ -140,6 +150,7 @@ class Engine:
         B, T, H, W, C = video.shape
         if C != 3:
             raise ValueError("inputs must have 3 channels")
+        _check_device(video, self.device, "video")
         video = video.contiguous()
         if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
             video = video.float()
@@ -156,6 +167,12 @@ class Engine:
             self._grids.add((H, W))
         if out is None:
             out = torch.empty((B, T * N, D), dtype=out_dtype, device=video.device)
+        else:  # the kernels write B*T*N*D elements through the raw pointer
+            _check_device(out, self.device, "out")
+            if tuple(out.shape) != (B, T * N, D) or out.dtype not in (torch.bfloat16, torch.float32) \
+                    or not out.is_contiguous():
+                raise ValueError(f"out must be a contiguous bf16/fp32 tensor of shape {(B, T * N, D)}, "
+                                 f"got {tuple(out.shape)} {out.dtype} contiguous={out.is_contiguous()}")
         sp = torch.empty_like(out) if want_spatial else None
         fp = None
         if frame_paddings is not None:
@@ -332,6 +349,9 @@ class ClipEngine:
     def profile_only(self, names=None) -> None:
         _profile_set_mask(self.video_handle(), names)
 
+    def kernel_name(self, cls_name: str) -> str:
+        return _native.profile_kernel_name(self.video_handle(), cls_name)
+
     def _workspace(self, key, nbytes):
         torch = _torch()
         ws = self._ws.get(key)
@@ -351,6 +371,7 @@ class ClipEngine:
         if H % P or W % P:
             raise ValueError(f"Image height ({H}) and width ({W}) should be multiples "
                              f"of patch_size ({P}).")
+        _check_device(video, self.device, "video")
         video = video.contiguous()
         if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
             video = video.float()
@@ -385,6 +406,7 @@ class ClipEngine:
     def encode_text(self, ids, paddings, normalize=True, stream=None):
         torch = _torch()
         Q, L = ids.shape
+        _check_device(ids, self.device, "text_token_ids")
         ids = ids.to(dtype=torch.int32).contiguous()
         pad = paddings.to(device=ids.device, dtype=torch.float32).contiguous()
         if tuple(pad.shape) != (Q, L):
@@ -581,6 +603,7 @@ class ClassifierEngine:
         if H % P or W % P:
             raise ValueError(f"Image height ({H}) and width ({W}) should be multiples "
                              f"of patch_size ({P}).")
+        _check_device(video, self.device, "video")
         video = video.contiguous()
         if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
             video = video.float()

@@ -178,6 +178,8 @@ def canonical_params(variables) -> dict[str, np.ndarray]:
         flat[k] = v
     if any(re.search(r"/layers/\d+/", k) for k in flat) or any(re.search(r"/x_layers_\d+/", k) for k in flat):
         flat = _restack(flat)
+    elif any(k.endswith("/weight") for k in flat):  # renamed but still stacked
+        flat = {_mlx_rename(k): v for k, v in flat.items()}
     return {k: _to_f32(v) for k, v in flat.items()}
 
 
@@ -191,13 +193,24 @@ def _to_f32(v) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(v, dtype=np.float32))
 
 
+# inverse of convert_weights.py:88-104 rename_parameter ('/kernel', '/scale', '/emb_var' ->
+# '/weight'), by leaf; token_emb is the one the reference's own loader maps back explicitly
+# (weight_utils.py:33-34)
 _MLX_RENAMES = (
     ("patch_projection/linear/weight", "patch_projection/linear/kernel"),
     ("pos_emb/weight", "pos_emb/emb_var"),
+    ("token_emb/weight", "token_emb/emb_var"),
     ("linear/weight", "linear/kernel"),
     ("layer_norm/weight", "layer_norm/scale"),
     ("_ln/weight", "_ln/scale"),
 )
+
+
+def _mlx_rename(k: str) -> str:
+    for a, b in _MLX_RENAMES:
+        if k.endswith(a):
+            return k[: -len(a)] + b
+    return k
 
 
 def _restack(flat: dict) -> dict:
@@ -206,10 +219,7 @@ def _restack(flat: dict) -> dict:
     groups: dict[tuple[str, str], dict[int, np.ndarray]] = {}
     out = {}
     for k, v in flat.items():
-        for a, b in _MLX_RENAMES:
-            if k.endswith(a):
-                k = k[: -len(a)] + b
-                break
+        k = _mlx_rename(k)
         m = re.match(r"^(.*)/(?:layers/(\d+)|x_layers_(\d+))/(.*)$", k)
         if m:
             idx = int(m.group(2) if m.group(2) is not None else m.group(3))
