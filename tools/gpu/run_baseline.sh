@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r2s2_gputest.log 2>&1 && \
+timeout -k 10 300 python -u tools/gemm_bench.py fold > gpurun_out/r2s2_gemm_fold.log 2>&1 && \
+timeout -k 10 300 python -u bench.py > gpurun_out/r2s2_bench.log 2>&1

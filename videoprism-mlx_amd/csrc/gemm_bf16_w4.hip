@@ -343,15 +343,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         v.lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
         v.hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
         if constexpr (Tr::kLn) {  // LN(x) . W + b = rstd * (x . W') - mean*rstd * c + b'
-          const float r = rs[mt][pass].x, q = rs[mt][pass].y;
-          v.lo.x = fmaf(r, v.lo.x, fmaf(q, cl[nh].x, bl[nh].x));
-          v.lo.y = fmaf(r, v.lo.y, fmaf(q, cl[nh].y, bl[nh].y));
-          v.lo.z = fmaf(r, v.lo.z, fmaf(q, cl[nh].z, bl[nh].z));
-          v.lo.w = fmaf(r, v.lo.w, fmaf(q, cl[nh].w, bl[nh].w));
-          v.hi.x = fmaf(r, v.hi.x, fmaf(q, ch[nh].x, bh[nh].x));
-          v.hi.y = fmaf(r, v.hi.y, fmaf(q, ch[nh].y, bh[nh].y));
-          v.hi.z = fmaf(r, v.hi.z, fmaf(q, ch[nh].z, bh[nh].z));
-          v.hi.w = fmaf(r, v.hi.w, fmaf(q, ch[nh].w, bh[nh].w));
+          // packed pairs (v_pk_fma_f32): the same two roundings per value as the scalar form
+          const f32x2_t r = f32x2_t(rs[mt][pass].x), q = f32x2_t(rs[mt][pass].y);
+          auto fold2 = [&](float& x0, float& x1, float c0, float c1, float b0, float b1) {
+            const f32x2_t o = __builtin_elementwise_fma(
+                r, f32x2_t{x0, x1}, __builtin_elementwise_fma(q, f32x2_t{c0, c1}, f32x2_t{b0, b1}));
+            x0 = o.x;
+            x1 = o.y;
+          };
+          fold2(v.lo.x, v.lo.y, cl[nh].x, cl[nh].y, bl[nh].x, bl[nh].y);
+          fold2(v.lo.z, v.lo.w, cl[nh].z, cl[nh].w, bl[nh].z, bl[nh].w);
+          fold2(v.hi.x, v.hi.y, ch[nh].x, ch[nh].y, bh[nh].x, bh[nh].y);
+          fold2(v.hi.z, v.hi.w, ch[nh].z, ch[nh].w, bh[nh].z, bh[nh].w);
         } else {
           v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
           v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;

@@ -32,23 +32,55 @@ struct EpiTraits {
   static constexpr bool kOutBf16 = !(EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN || EPI == EPI_POS_F32);
 };
 
-// A&S 7.1.26 erf (|err| <= 1.5e-7) folded into GELU: 0.5*(x + |x|*erf(|x|/sqrt2)).
+// GELU(x) = x * Phi(x) (exact-erf form, layers.py:31) in one transcendental:
+//   gelu(x) = max(x, 0) - t * Phi(-t),   t = min(|x|, GELU_TMAX),
+//   Phi(-t) = exp2(P(t)),  P = degree-7 fit of log2 Phi(-t) on [0, 5.6] (tools/fit_gelu.py log2).
+// fp32 result vs x*Phi(x) in fp64: relative error <= 5.7e-6, absolute <= 9.6e-7 (checked on
+// [-30, 30] with fp32 Horner); beyond |x| = 5.6 the clamped term is below 6e-8.  Per value pair:
+// 2 min, 7 packed FMA, 2 exp2, 2 max, 1 packed FMA = 12 VALU + 2 transcendental issues (the
+// former A&S 7.1.26 form needed 13 + 4: an rcp and an exp2 per value).
+constexpr float GELU_TMAX = 5.6f;
+#define VP_GELU_P7 -1.8099689214068349e-06f
+#define VP_GELU_P6 6.117992597864941e-05f
+#define VP_GELU_P5 -0.0009278103243559599f
+#define VP_GELU_P4 0.00849936343729496f
+#define VP_GELU_P3 -0.05394672974944115f
+#define VP_GELU_P2 -0.45847392082214355f
+#define VP_GELU_P1 -1.1512486934661865f
+#define VP_GELU_P0 -0.9999953508377075f
+
 __device__ __forceinline__ float gelu_fast(float x) {
-  const float ax = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
-  float p = fmaf(t, 1.061405429f, -1.453152027f);
-  p = fmaf(t, p, 1.421413741f);
-  p = fmaf(t, p, -0.284496736f);
-  p = fmaf(t, p, 0.254829592f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f(x * x * (-0.5f * 1.4426950408889634f));
-  return 0.5f * fmaf(ax, fmaf(-p, e, 1.0f), x);
+  const float t = __builtin_fminf(__builtin_fabsf(x), GELU_TMAX);
+  float p = fmaf(t, VP_GELU_P7, VP_GELU_P6);
+  p = fmaf(t, p, VP_GELU_P5);
+  p = fmaf(t, p, VP_GELU_P4);
+  p = fmaf(t, p, VP_GELU_P3);
+  p = fmaf(t, p, VP_GELU_P2);
+  p = fmaf(t, p, VP_GELU_P1);
+  p = fmaf(t, p, VP_GELU_P0);
+  return fmaf(-t, __builtin_amdgcn_exp2f(p), __builtin_fmaxf(x, 0.0f));
 }
 
-// The same operation sequence on two values with packed fp32 math (v_pk_fma_f32 /
-// v_pk_mul_f32): bit-identical to two gelu_fast calls, half the VALU issue slots.
+// The same operation sequence on two values with packed fp32 math (v_pk_fma_f32):
+// bit-identical to two gelu_fast calls, fewer VALU issue slots.
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t x) {
+  const f32x2_t t = {__builtin_fminf(__builtin_fabsf(x.x), GELU_TMAX), __builtin_fminf(__builtin_fabsf(x.y), GELU_TMAX)};
+  f32x2_t p = __builtin_elementwise_fma(t, f32x2_t(VP_GELU_P7), f32x2_t(VP_GELU_P6));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P5));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P4));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P3));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P2));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P1));
+  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P0));
+  const f32x2_t e = {__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
+  const f32x2_t m = {__builtin_fmaxf(x.x, 0.0f), __builtin_fmaxf(x.y, 0.0f)};
+  return __builtin_elementwise_fma(-t, e, m);
+}
+
+// The former two-transcendental form (A&S 7.1.26 erf, |err| <= 1.5e-7), kept for the A/B build
+// of the ffn_layer1 epilogue (DIAG 1024 in gemm_bf16_w4.hip).
+__device__ __forceinline__ f32x2_t gelu_as2(f32x2_t x) {
   const f32x2_t ax = {fabsf(x.x), fabsf(x.y)};
   const f32x2_t d = __builtin_elementwise_fma(f32x2_t(0.3275911f * 0.70710678118654752f), ax, f32x2_t(1.0f));
   const f32x2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
@@ -140,8 +172,12 @@ __device__ __forceinline__ F8 epi_extra8(const EpiArgs& ep, int row, int n, int 
 
 __device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, bool gelu, bool kp, bool ex,
                                            bool relu = false, bool scalar_gelu = false) {
-  if (gelu && scalar_gelu) v = make_float4(gelu_fast(v.x), gelu_fast(v.y), gelu_fast(v.z), gelu_fast(v.w));
-  else if (gelu) v = gelu4(v);
+  if (gelu && scalar_gelu) {  // A/B only: the former A&S form
+    const f32x2_t a = gelu_as2(f32x2_t{v.x, v.y}), b = gelu_as2(f32x2_t{v.z, v.w});
+    v = make_float4(a.x, a.y, b.x, b.y);
+  } else if (gelu) {
+    v = gelu4(v);
+  }
   if (relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
   if (kp) { v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep; }
   if (ex) { v.x += extra.x; v.y += extra.y; v.z += extra.z; v.w += extra.w; }
