@@ -38,7 +38,7 @@ def horner32(c, a):
 def main():
     a = np.linspace(0.0, AMAX, 40001)
     R = 0.5 * erfc(a / np.sqrt(2.0)) * np.exp(a * a / 2.0)
-    want = int(sys.argv[1]) if len(sys.argv) > 1 else None
+    want = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else None
     for deg in range(5, 12):
         c = fit(deg, a, R)
         e32 = np.abs((horner32(c, a) - R) / R).max()
@@ -60,6 +60,36 @@ def fit_tanh(y0=0.48, deg=3):
     c = fit(deg, v, T)
     err = np.abs((horner32(c, v) - T) / T).max()
     return c, err
+
+
+def fit_log2(deg=7, tmax=5.6):
+    """Production GELU epilogue (gemm_epilogue.h gelu_fast2): P(t) ~ log2 Phi(-t) on [0, tmax],
+    gelu(x) = max(x, 0) - t * exp2(P(t)), t = min(|x|, tmax).  Returns the coefficients and the
+    fp32 relative / absolute error of the whole GELU against x*Phi(x) on [-30, 30]."""
+    from scipy.special import log_ndtr, ndtr
+    t = np.linspace(0.0, tmax, 40001)
+    f = log_ndtr(-t) / np.log(2.0)
+    V = np.vander(t, deg + 1, increasing=True)
+    ww = np.ones_like(t)
+    for _ in range(60):
+        c, *_ = np.linalg.lstsq(V * ww[:, None], f * ww, rcond=None)
+        err = V @ c - f
+        ww = ww * (1.0 + np.abs(err) / np.abs(err).max()) ** 2
+        ww /= ww.max()
+    x = np.concatenate([np.linspace(-30, 30, 600001), np.linspace(-6, 6, 400001)]).astype(np.float32)
+    tt = np.minimum(np.abs(x), np.float32(tmax))
+    p = horner32(c, tt.astype(np.float64)).astype(np.float32)
+    g = (np.maximum(x, np.float32(0)) - tt * np.exp2(p).astype(np.float32)).astype(np.float64)
+    gt = x.astype(np.float64) * ndtr(x.astype(np.float64))
+    e = np.abs(g - gt)
+    m = np.abs(gt) > 1e-6
+    return c, float((e[m] / np.abs(gt[m])).max()), float(e.max())
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "log2":
+    for deg in (6, 7, 8):
+        c, rel, ab = fit_log2(deg)
+        print(f"log2 form degree {deg}: rel {rel:.2e} abs {ab:.2e}:", ", ".join(f"{float(np.float32(v))!r}f" for v in c))
 
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "tanh":
