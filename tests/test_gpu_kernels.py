@@ -415,3 +415,4 @@ def test_gemm_row_stats(cuda, epi):
     ref = torch.stack([rstd, -mean * rstd], 1)
     assert torch.allclose(rs_p.double(), ref, rtol=2e-5, atol=1e-5)
     assert torch.allclose(rs_r.double(), ref, rtol=2e-5, atol=1e-5)
+

@@ -515,6 +515,25 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
 }
 
 #ifdef VP_DIAG
+// diag library only: the fused q|k|v projection + spatial attention kernel (an experiment that
+// measured no faster than the unfused pair; tools/qa_bench.py checks it bitwise
+// against vp_dev_gemm_ln(EPI_BF16_LN) + vp_op_attention)
+int vp_dev_qkv_attention(const void* x, const float* ln_rs, const void* wqkv, const float* bias,
+                         const float* lnc, void* out, int64_t frames, int64_t heads, float cap, void* stream) {
+  using namespace vp;
+  if (!qkv_attention_spatial_ok((int)frames, (int)heads, cap < -1000.f ? 50.f : cap))
+    return fail(VP_EINVAL, "qkv_attention: needs heads*64 == 768, cap > 0 and frames*256 rows in range");
+  if (cap < -1000.f) {  // ablation builds: cap = -1000 - diag (tools/qa_bench.py)
+    VP_HIP(qkv_attention_spatial_diag((int)(-1000.f - cap), (const bf16_t*)x, ln_rs, (const bf16_t*)wqkv, bias,
+                                      lnc, (bf16_t*)out, (int)frames, (int)heads, 50.f,
+                                      static_cast<hipStream_t>(stream)));
+    return VP_OK;
+  }
+  VP_HIP(qkv_attention_spatial_bf16((const bf16_t*)x, ln_rs, (const bf16_t*)wqkv, bias, lnc, (bf16_t*)out,
+                                    (int)frames, (int)heads, cap, static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // ablation builds of the spatial attention kernel (tools/attn_bench.py)
 int vp_dev_attention_diag(int diag, const void* qkv, void* o, int64_t num_seq, int64_t heads, float cap,
                           void* stream) {

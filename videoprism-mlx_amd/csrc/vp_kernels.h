@@ -85,6 +85,17 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
 // ---- attention (attention.hip) ----
 // qkv: rows of [q(D) | k(D) | v(D)], row r = seq * S + s; q pre-scaled by dh^-0.5.
 // o: rows of D = heads*64.  key_pad: optional [num_seq * S] (1 = padded key).
+// diag library only (A/B experiment, measured no faster than the unfused pair):
+// q|k|v projection (LN1 folded, EPI_BF16_LN arithmetic) + spatial attention (S = 256, dh = 64,
+// D = 768, no key paddings) fused per (frame, head) (qkv_attention.hip); bitwise equal to
+// gemm_bf16_w4(EPI_BF16_LN) followed by attention_spatial_bf16.
+bool qkv_attention_spatial_ok(int frames, int heads, float cap);
+hipError_t qkv_attention_spatial_bf16(const bf16_t* x, const float* ln_rs, const bf16_t* wqkv, const float* bias,
+                                      const float* lnc, bf16_t* o, int frames, int heads, float cap,
+                                      hipStream_t s);
+hipError_t qkv_attention_spatial_diag(int diag, const bf16_t* x, const float* ln_rs, const bf16_t* wqkv,
+                                      const float* bias, const float* lnc, bf16_t* o, int frames, int heads,
+                                      float cap, hipStream_t s);
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, const float* key_pad, hipStream_t s);
 // [diag library only] ablation builds of the spatial kernel (tools/attn_bench.py)

@@ -145,6 +145,8 @@ _DIAG_SIGNATURES = {
     "vp_dev_attention_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                  c_void_p, c_void_p]),
+    "vp_dev_qkv_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_int64, c_int64, c_float, c_void_p]),
 }
 
 _lib = None
@@ -267,6 +269,14 @@ def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln
     call("vp_dev_gemm_ln", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
          _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad), _ptr(ln_rs), _ptr(ln_c),
          _ptr(st_part), _stream(stream))
+    return out
+
+
+def dev_qkv_attention(x, ln_rs, wqkv, bias, lnc, out, frames, heads, cap, stream=None):
+    """Fused q|k|v projection (LN1 folded) + spatial attention: x [frames*256, D] bf16 ->
+    out [frames*256, D] bf16; all tensors contiguous on the device."""
+    call("vp_dev_qkv_attention", _ptr(x), _ptr(ln_rs), _ptr(wqkv), _ptr(bias), _ptr(lnc), _ptr(out),
+         frames, heads, float(cap), _stream(stream))
     return out
 
 
