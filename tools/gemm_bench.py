@@ -130,12 +130,31 @@ def folded(dev, g):
                                                           for k, v in res.items()), flush=True)
 
 
+def msize(dev, g):
+    """ffn_layer2 / ffn_layer1 at smaller M (A resident in the 256 MiB Infinity Cache when it fits):
+    per-FLOP rate vs the B=32 shape (forward epilogues, isolated back-to-back launches)."""
+    for name, N, K, epi in (("ffn2", 768, 3072, nat.EPI_RESID_FFN_BF16_ST), ("ffn1", 3072, 768, nat.EPI_GELU_LN)):
+        for M in (131072, 65536, 32768):
+            a, w, b = operands(M, N, K, g, dev)
+            rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
+            c = torch.zeros(N, device=dev)
+            part = torch.empty((N // 128, M, 2), device=dev)
+            o = torch.zeros((M, N), device=dev, dtype=torch.bfloat16)
+            resid = epi == nat.EPI_RESID_FFN_BF16_ST
+            f = lambda: nat.dev_gemm_ln(a, w, b, epi, o, resid=o if resid else None, ln_rs=rs, ln_c=c, st_part=part)
+            t = min(timeit(f) for _ in range(3))
+            print(f"{name} M={M}: {t*1e3:7.1f} us {2.0*M*N*K/t/1e9:7.1f} TF", flush=True)
+            del a, o, part, rs
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
     if mode == "fold":
         folded(dev, g)
+    elif mode == "msize":
+        msize(dev, g)
     elif mode == "early":
         variants(dev, g, 4, [0, 1024, 2048, 4096])
     elif mode == "nt":
