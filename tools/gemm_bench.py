@@ -147,12 +147,35 @@ def msize(dev, g):
             del a, o, part, rs
 
 
+def skew(dev, g):
+    """Start skew (DIAG 64, EPI_BF16): workgroup group (b>>3) % G of every XCD delays its first
+    K-tile by group * d, so the CUs' epilogue store bursts stop coinciding (G, d swept)."""
+    cfgs = [(1, 0), (2, 400), (2, 800), (2, 1200), (4, 300), (4, 600), (8, 150), (8, 300)]
+    for name, M, N, K, _ in SHAPES:
+        a, w, b = operands(M, N, K, g, dev)
+        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        res = {c: [] for c in [None] + cfgs}
+        for _ in range(3):
+            for c in res:
+                if c is None:
+                    f = lambda: nat.dev_gemm_kernel(4, a, w, b, 0, o)
+                else:
+                    pos = torch.empty(c[0] * 10000 + c[1], device=dev)
+                    f = lambda: nat.dev_gemm_kernel(4, a, w, b, 1064, o, pos=pos)
+                res[c].append(timeit(f, iters=10, warm=2))
+        print(f"{name} skew (G, d x10ns):", " ".join(f"{c}:{min(t)*1e3:6.1f}" for c, t in res.items()), flush=True)
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
     if mode == "fold":
         folded(dev, g)
+    elif mode == "epilds":
+        variants(dev, g, 4, [0, 8, 32, 5000, 5001, 5002, 5003])
+    elif mode == "skew":
+        skew(dev, g)
     elif mode == "msize":
         msize(dev, g)
     elif mode == "early":

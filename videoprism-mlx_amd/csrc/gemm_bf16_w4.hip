@@ -53,11 +53,12 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // run time; the accumulators stay live), 16 = after an epilogue the next barrier waits vmcnt(32)
 // (lets the stores drain behind the next tile; correct, measured no faster), 32 = epilogue
 // without its global stores (LDS transposition and math kept), 64 = start skew: workgroup
-// group (b>>3)&3 of every XCD waits group * nk * 0.5 us (~a quarter tile) before its first
-// K-tile, so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
+// group (b>>3) % G of every XCD waits group * d before its first K-tile (G, d from
+// ep.pos_rows), so the tiles' epilogue store bursts do not coincide across the chip, 128 = h1
 // schedule with the 16 loads and 16 reads in its first 32 MFMAs, 256 = plain (temporal) output stores,
 // 512 (production) = no padded rows: the epilogue skips the (1 - rowpad) factor, 1024 = GELU in
-// unpacked fp32 arithmetic (A/B).
+// unpacked fp32 arithmetic (A/B), 2048 / 4096 = epilogue without the LDS transposition's
+// writes / read-backs.
 // PF > 0: L2 prefetch of A, PF K-tiles beyond the K-tile being staged (one dword per A row per
 // K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  Pays where A streams
 // from HBM (ffn_layer2, K = 3072: 490 -> 471 us); costs on the K = 768 shapes (A mostly from the
@@ -245,7 +246,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
 
   int g = 0;
   if constexpr (DIAG & 64) {
-    const uint64_t ticks = (uint64_t)((b >> 3) & 3) * nk * 50;  // s_memrealtime runs at 100 MHz
+    // ep.pos_rows (unused by EPI_BF16) = groups * 10000 + delay per group in 10-ns ticks
+    const int ng = ep.pos_rows / 10000 > 0 ? ep.pos_rows / 10000 : 1;
+    const uint64_t ticks = (uint64_t)((b >> 3) % ng) * (uint64_t)(ep.pos_rows % 10000);  // s_memrealtime: 100 MHz
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
   }
@@ -312,6 +315,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     // block G = (mt, nh): acc[nh*4 + q][mt], q = 0..3 -> scratch buffer G & 1.  Block G+1 is
     // written before block G is read back, so the LDS round trip overlaps the math and stores.
     auto put = [&](int G) {
+      if constexpr (DIAG & 2048) {
+        if (ep.ldo != -12345) return;  // never false at run time: ablation without the LDS writes
+      }
       const int mt = G >> 1, nh = G & 1;
       char* sb = scr + (G & 1) * kScrBuf + frow * 256;
 #pragma unroll
@@ -340,8 +346,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         const int n = n0 + nh * 64 + es * 8;
         const char* sb = scr + (G & 1) * kScrBuf + rl * 256;
         F8 v;
-        v.lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
-        v.hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
+        if ((DIAG & 4096) && ep.ldo != -12345) {  // ablation without the LDS read-back
+          v.lo = make_float4((float)G, (float)pass, (float)rl, 0.f);
+          v.hi = v.lo;
+        } else {
+          v.lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
+          v.hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
+        }
         if constexpr (Tr::kLn) {  // LN(x) . W + b = rstd * (x . W') - mean*rstd * c + b'
           // packed pairs (v_pk_fma_f32): the same two roundings per value as the scalar form
           const f32x2_t r = f32x2_t(rs[mt][pass].x), q = f32x2_t(rs[mt][pass].y);
@@ -505,6 +516,10 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 128: return launch_w4<EPI_BF16, 128>(A, lda, W, ldw, M, N, K, ep, s);
       case 136: return launch_w4<EPI_BF16, 136>(A, lda, W, ldw, M, N, K, ep, s);
       case 256: return launch_w4<EPI_BF16, 256>(A, lda, W, ldw, M, N, K, ep, s);
+      case 5000: return launch_w4<EPI_BF16, 2048>(A, lda, W, ldw, M, N, K, ep, s);
+      case 5001: return launch_w4<EPI_BF16, 4096>(A, lda, W, ldw, M, N, K, ep, s);
+      case 5002: return launch_w4<EPI_BF16, 6144>(A, lda, W, ldw, M, N, K, ep, s);
+      case 5003: return launch_w4<EPI_BF16, 6144 | 32>(A, lda, W, ldw, M, N, K, ep, s);
       case 1024: return launch_w4<EPI_BF16, 0, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 2048: return launch_w4<EPI_BF16, 0, 3>(A, lda, W, ldw, M, N, K, ep, s);
       case 4096: return launch_w4<EPI_BF16, 0, 4>(A, lda, W, ldw, M, N, K, ep, s);

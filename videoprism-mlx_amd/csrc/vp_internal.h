@@ -422,6 +422,22 @@ enum AttnKind {
 };
 
 // One forward pass's launch context: stream, dtype, row count, scratch buffers and the profiler.
+// hipEventRecord on `s`; inside a stream capture an event-record node of the graph instead (a
+// plain record during capture only orders the capture, so a replay would not re-record it)
+inline hipError_t record_event(hipEvent_t ev, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  hipError_t e = hipStreamGetCaptureInfo_v2(s, &cs, nullptr, &g, &deps, &nd);
+  if (e != hipSuccess) return e;
+  if (cs != hipStreamCaptureStatusActive) return hipEventRecord(ev, s);
+  hipGraphNode_t node = nullptr;
+  e = hipGraphAddEventRecordNode(&node, g, deps, nd, ev);
+  if (e != hipSuccess) return e;
+  return hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+}
+
 struct Fwd {
   hipStream_t s = nullptr;
   bool bf = false;
@@ -446,12 +462,12 @@ struct Fwd {
     };
     if (!pf || pf->used >= pf->cap || !((pf->mask >> cls) & 1u)) return launch();
     const int i = pf->used++;
-    hipError_t e = hipEventRecord(pf->ev[2 * i], s);
+    hipError_t e = record_event(pf->ev[2 * i], s);
     if (e != hipSuccess) return e;
     e = launch();
     if (e != hipSuccess) return e;
     pf->cls[i] = cls; pf->flops[i] = flops; pf->bytes[i] = bytes;
-    return hipEventRecord(pf->ev[2 * i + 1], s);
+    return record_event(pf->ev[2 * i + 1], s);
   }
 
   hipError_t gemm(int epi, const void* A, int K, const void* Wt, int N, void* o, int64_t ldo, const float* bias,
