@@ -41,11 +41,17 @@ def main():
     fns = {f"d{d}": (lambda d=d: nat.call("vp_dev_attention_diag", d, qkv.data_ptr(), o.data_ptr(), nseq,
                                           heads, 50.0, st())) for d in diags}
     fns["prod"] = lambda: nat.op_attention(qkv, nseq, S, heads, 50.0, out=o)
+    # streaming reference: read the q|k|v buffer and write a same-size copy (2 x 604 MB)
+    cp = torch.empty_like(qkv)
+    fns["copy"] = lambda: cp.copy_(qkv)
     res = {k: [] for k in fns}
     for _ in range(3):
         for k, f in fns.items():
             res[k].append(timeit(f))
     flop = 4.0 * nseq * S * S * D
+    nbytes = qkv.numel() * 2
+    print(f"copy of q|k|v: {2 * nbytes / min(res['copy']) / 1e6:.0f} GB/s; attention bytes "
+          f"{(nbytes + o.numel() * 2) / 1e6:.0f} MB", flush=True)
     print("spatial attention:", " ".join(f"{k}: {min(v)*1e3:6.1f} us ({flop/min(v)/1e9:5.0f} TF)"
                                         for k, v in res.items()), flush=True)
 

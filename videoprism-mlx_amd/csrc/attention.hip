@@ -85,7 +85,19 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   const int q0 = w * 32;
   const int half = lane >> 5;
   bf16x8 qf[4];
-  {
+  if constexpr ((DIAG & 64) != 0) {  // ablation: no Q loads
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) {
+      qf[kd] = bf16x8{};
+      asm volatile("" : "+v"(qf[kd]));
+    }
+  } else if constexpr ((DIAG & 8) != 0) {  // ablation: Q by whole 128-B lines (8 rows per load)
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) {
+      const bf16_t* qp = base + (int64_t)(q0 + kd * 8 + (lane >> 3)) * ld + 8 * (lane & 7);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qp));
+    }
+  } else {
     const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
 #pragma unroll
     for (int kd = 0; kd < 4; ++kd)
@@ -102,7 +114,8 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       const int row = (piece & 31) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
       const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * sec : sec) + c * 8;
-      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
+      if constexpr ((DIAG & 128) == 0)  // ablation 128: no K/V staging
+        __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
     }
   if constexpr (MASK) {  // (padded batches: no streaming)
     if (threadIdx.x < kSpS) kp[threadIdx.x] = key_pad[(int64_t)seq * kSpS + threadIdx.x];
@@ -483,11 +496,19 @@ hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int nu
   };
   if (diag == 4 + 32)  // staged stores + polynomial numerator
     return go((const void*)attn_spatial_kernel<false, 4, true>, attn_spatial_kernel<false, 4, true>);
-  if (diag >= 16) {
+  if (diag >= 16 && diag < 1000) {
     if (diag & 32) return go((const void*)attn_spatial_kernel<false, 0, true>, attn_spatial_kernel<false, 0, true>);
     return go((const void*)attn_spatial_kernel<false, 0, false>, attn_spatial_kernel<false, 0, false>);
   }
   switch (diag) {
+    // memory-pattern ablations on the production (staged-store) build: 8 = Q by whole lines,
+    // 64 = no Q loads, 128 = no K/V staging; | 3 = no numerators, no P.V
+    case 1000 + 3: return go((const void*)attn_spatial_kernel<false, 3, true>, attn_spatial_kernel<false, 3, true>);
+    case 1000 + 8: return go((const void*)attn_spatial_kernel<false, 8, true>, attn_spatial_kernel<false, 8, true>);
+    case 1000 + 11: return go((const void*)attn_spatial_kernel<false, 11, true>, attn_spatial_kernel<false, 11, true>);
+    case 1000 + 67: return go((const void*)attn_spatial_kernel<false, 67, true>, attn_spatial_kernel<false, 67, true>);
+    case 1000 + 131: return go((const void*)attn_spatial_kernel<false, 131, true>, attn_spatial_kernel<false, 131, true>);
+    case 1000 + 195: return go((const void*)attn_spatial_kernel<false, 195, true>, attn_spatial_kernel<false, 195, true>);
     case 0: return go((const void*)attn_spatial_kernel<false, 0>, attn_spatial_kernel<false, 0>);
     case 1: return go((const void*)attn_spatial_kernel<false, 1>, attn_spatial_kernel<false, 1>);
     case 2: return go((const void*)attn_spatial_kernel<false, 2>, attn_spatial_kernel<false, 2>);
