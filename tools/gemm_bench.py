@@ -166,6 +166,29 @@ def skew(dev, g):
         print(f"{name} skew (G, d x10ns):", " ".join(f"{c}:{min(t)*1e3:6.1f}" for c, t in res.items()), flush=True)
 
 
+def grouped(dev, g):
+    """ffn_layer1 (production LN-folded GELU epilogue) with the N-tile grouped tile order
+    (w4_ngrp) vs the ungrouped one (diag 3011), M = 131072 and the Large shape."""
+    for name, M, N, K in (("ffn1-base", M_TOK, 3072, 768), ("ffn1-large", 65536, 4096, 1024),
+                          ("qkv-large", 65536, 3072, 1024)):
+        a, w, b = operands(M, N, K, g, dev)
+        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
+        c = torch.zeros(N, device=dev)
+        epi = nat.EPI_GELU_LN if name.startswith("ffn1") else nat.EPI_BF16_LN
+        fns = {"grouped": lambda: nat.dev_gemm_ln(a, w, b, epi, o, ln_rs=rs, ln_c=c)}
+        if epi == nat.EPI_GELU_LN:
+            fns["ungrouped"] = lambda: nat.dev_gemm_ln(a, w, b, 3011, o, ln_rs=rs, ln_c=c)
+        res = {k: [] for k in fns}
+        for _ in range(3):
+            for k, f in fns.items():
+                res[k].append(timeit(f))
+        flop = 2.0 * M * N * K
+        print(f"{name}: " + " | ".join(f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()),
+              flush=True)
+        del a, o
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -174,6 +197,8 @@ def main():
         folded(dev, g)
     elif mode == "epilds":
         variants(dev, g, 4, [0, 8, 32, 5000, 5001, 5002, 5003])
+    elif mode == "grouped":
+        grouped(dev, g)
     elif mode == "skew":
         skew(dev, g)
     elif mode == "msize":

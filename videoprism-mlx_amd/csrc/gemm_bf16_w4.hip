@@ -66,10 +66,29 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 template <int EPI, int DIAG = 0, int PF = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
-    int N, int K, EpiArgs ep) {
+    int N, int K, int ngrp, EpiArgs ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = N / BN;
   const int T = (M / BM) * tilesN;
+  // tile index -> (M-block, N-tile).  ngrp == tilesN: N-tile fastest.  ngrp < tilesN (host: only
+  // when every XCD owns whole M-blocks): each XCD sweeps its M-blocks once per group of ngrp
+  // N-tiles, so the group's W rows (<= 2.5 MB) stay in the XCD's 4 MiB L2 instead of the whole W
+  // being re-fetched from beyond it for every M-block (ffn_layer1: W = 4.7 MB)
+  auto coords = [&](int t, int& tm, int& tn) {
+    if (ngrp == tilesN) {
+      tm = t / tilesN;
+      tn = t - tm * tilesN;
+      return;
+    }
+    const int mbx = (M / BM) >> 3;
+    const int x = t / (mbx * tilesN);
+    const int u = t - x * mbx * tilesN;
+    const int gsz = mbx * ngrp;
+    const int gi = u / gsz, r = u - gi * gsz;
+    const int rm = r / ngrp;
+    tm = x * mbx + rm;
+    tn = gi * ngrp + (r - rm * ngrp);
+  };
   const int G = gridDim.x;
   const int b = blockIdx.x;
   int first, stride, count;
@@ -107,15 +126,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // load stream: K-tile ld_g -> (tile ld_tm/ld_tn, K-tile ld_kt); the tail re-loads the last
   // K-tile (harmless), so every wait count stays uniform
   int ld_g = 0, ld_kt = 0, ld_tile = first;
-  int ld_tm = ld_tile / tilesN, ld_tn = ld_tile - ld_tm * tilesN;
+  int ld_tm, ld_tn;
+  coords(ld_tile, ld_tm, ld_tn);
   auto advance = [&]() {
     if (ld_g + 1 >= total) return;
     ++ld_g;
     if (++ld_kt == nk) {
       ld_kt = 0;
       ld_tile += stride;
-      ld_tm = ld_tile / tilesN;
-      ld_tn = ld_tile - ld_tm * tilesN;
+      coords(ld_tile, ld_tm, ld_tn);
     }
   };
   auto stage_piece = [&](int buf, int p) {  // p: 0..7 A pieces, 8..15 W pieces
@@ -261,8 +280,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     float4 cl[2], ch[2];  // EPI_*_LN: column sums of W'
     float2 rs[8][2];      // EPI_*_LN: (rstd, -mean*rstd) of rows mt*16 + pass*8 + er
     {
-      const int tile = first + j * stride;
-      const int nb = (tile % tilesN) * BN + wn * 128 + es * 8;
+      int ttm, ttn;
+      coords(first + j * stride, ttm, ttn);
+      const int nb = ttn * BN + wn * 128 + es * 8;
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) {
         bl[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64);
@@ -274,7 +294,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           cl[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64);
           ch[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64 + 4);
         }
-        const int mb = (tile / tilesN) * BM + wm * 128 + er;
+        const int mb = ttm * BM + wm * 128 + er;
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
@@ -298,8 +318,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     if constexpr (DIAG & 8) {
       if (ep.ldo != -12345) continue;  // never false at run time: keeps acc live, skips stores
     }
-    const int tile = first + j * stride;
-    const int m0 = (tile / tilesN) * BM + wm * 128, n0 = (tile % tilesN) * BN + wn * 128;
+    int etm, etn;
+    coords(first + j * stride, etm, etn);
+    const int m0 = etm * BM + wm * 128, n0 = etn * BN + wn * 128;
     using Tr = EpiTraits<EPI>;
     char* scr = smem + kLds + w * kScr;
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
@@ -434,6 +455,18 @@ int num_cus_w4() {
   return n;
 }
 
+// N-tile group size (see coords): the whole W when it fits an XCD's L2 with room to spare, or
+// when the GEMM streams A from HBM (K >= 2048: a group sweep would re-read A per group)
+int w4_ngrp(int M, int N, int K, int grid) {
+  const int tilesN = N / BN;
+  const int64_t w_tile = (int64_t)BN * K * 2;  // W bytes per N-tile
+  if ((int64_t)tilesN * w_tile <= (4ll << 20) || K >= 2048 || (M / BM) % 8 || grid % 8) return tilesN;
+  int g = tilesN;
+  for (int d = tilesN; d >= 1; --d)
+    if (tilesN % d == 0 && (int64_t)d * w_tile <= (5ll << 19)) { g = d; break; }
+  return g;
+}
+
 template <int EPI, int DIAG = 0, int PF = 0>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
@@ -446,9 +479,10 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
+  const int ngrp = (DIAG & 32768) ? N / BN : w4_ngrp(M, N, K, grid);  // DIAG 32768: ungrouped (A/B)
   VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF>));
   hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
-                     ldw, M, N, K, ep);
+                     ldw, M, N, K, ngrp, ep);
   return hipGetLastError();
 }
 
@@ -520,6 +554,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 5001: return launch_w4<EPI_BF16, 4096>(A, lda, W, ldw, M, N, K, ep, s);
       case 5002: return launch_w4<EPI_BF16, 6144>(A, lda, W, ldw, M, N, K, ep, s);
       case 5003: return launch_w4<EPI_BF16, 6144 | 32>(A, lda, W, ldw, M, N, K, ep, s);
+      // the ffn_layer1 production epilogue without the N-tile grouping (A/B of w4_ngrp)
+      case 2011: return launch_w4<EPI_GELU_BF16_LN, 512 | 32768>(A, lda, W, ldw, M, N, K, ep, s);
       case 1024: return launch_w4<EPI_BF16, 0, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 2048: return launch_w4<EPI_BF16, 0, 3>(A, lda, W, ldw, M, N, K, ep, s);
       case 4096: return launch_w4<EPI_BF16, 0, 4>(A, lda, W, ldw, M, N, K, ep, s);
