@@ -349,15 +349,22 @@ def op_pool_l2(emb, stream=None):
 
 
 def source_fingerprint() -> str:
-    """sha256 over the library's sources (csrc/ and include/): bench.py only quotes PMC traffic
-    measured on a build of exactly these sources."""
+    """sha256 over the product library's sources (the Makefile's SRC list, csrc/ headers and
+    include/): bench.py only quotes PMC traffic measured on a build of exactly these sources.
+    Files only the tools' diag library compiles (DIAG_SRC) do not count."""
     import hashlib
+    import re
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "csrc")
+    with open(os.path.join(root, "Makefile")) as fh:
+        m = re.search(r"^SRC\s*:=\s*(.+)$", fh.read(), re.M)
+    product = {os.path.basename(f) for f in m.group(1).split()} if m else None
     files = []
-    for d in (os.path.join(root, "csrc"), os.path.join(os.path.dirname(root), "include")):
+    for d in (csrc, os.path.join(os.path.dirname(root), "include")):
         if os.path.isdir(d):
             files += sorted(os.path.join(d, f) for f in os.listdir(d)
-                            if f.endswith((".hip", ".cpp", ".h")))
+                            if f.endswith(".h") or (f.endswith((".hip", ".cpp")) and
+                                                    (product is None or f in product)))
     h = hashlib.sha256()
     for f in files:
         h.update(os.path.basename(f).encode())
