@@ -41,6 +41,14 @@ def main():
     fns = {f"d{d}": (lambda d=d: nat.call("vp_dev_attention_diag", d, qkv.data_ptr(), o.data_ptr(), nseq,
                                           heads, 50.0, st())) for d in diags}
     fns["prod"] = lambda: nat.op_attention(qkv, nseq, S, heads, 50.0, out=o)
+    if os.environ.get("QH"):  # half-frame workgroups, K/V in two 128-key chunks (attention_qh.hip)
+        o2 = torch.empty_like(o)
+        nat.op_attention(qkv, nseq, S, heads, 50.0, out=o)
+        nat.call("vp_dev_attention_qh", qkv.data_ptr(), o2.data_ptr(), nseq, heads, 50.0, st())
+        torch.cuda.synchronize()
+        print("qh == prod (bitwise):", bool(torch.equal(o, o2)),
+              "max diff", float((o.float() - o2.float()).abs().max()), flush=True)
+        fns["qh"] = lambda: nat.call("vp_dev_attention_qh", qkv.data_ptr(), o2.data_ptr(), nseq, heads, 50.0, st())
     # streaming reference: read the q|k|v buffer and write a same-size copy (2 x 604 MB)
     cp = torch.empty_like(qkv)
     fns["copy"] = lambda: cp.copy_(qkv)

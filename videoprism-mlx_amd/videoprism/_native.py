@@ -143,6 +143,7 @@ _SIGNATURES = {
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
     "vp_dev_attention_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
+    "vp_dev_attention_qh": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                  c_void_p, c_void_p]),
     "vp_dev_qkv_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
