@@ -116,7 +116,9 @@ def test_gemm_bf16_pos_bf16(cuda):
 
 
 # both bf16 GEMM kernels on persistent shapes: tiles > CUs (several tiles per workgroup, so the
-# K-tile stream crosses tile boundaries), tile counts not divisible by 8 XCDs, K = 1..48 K-tiles
+# K-tile stream crosses tile boundaries), tile counts not divisible by 8 XCDs, K = 1..48 K-tiles;
+# (4096, 3072, 768) has W = 4.7 MB > an XCD's L2, so the 4-wave kernel runs it in the N-tile
+# grouped tile order (w4_ngrp: groups of 6 N-tiles, 192 workgroups) -- the same order as ffn_layer1
 KERNEL_SHAPES = [(16384, 2304, 768), (32768, 768, 3072), (2304, 1536, 64), (512, 256, 1024),
                  (4096, 3072, 768)]
 
