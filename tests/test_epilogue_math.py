@@ -1,8 +1,8 @@
 """The GEMM epilogue's GELU (videoprism-mlx_amd/csrc/gemm_epilogue.h gelu_fast2), restated in
 fp32 NumPy with the coefficients parsed from the header, against the exact-erf GELU of the
 reference (layers.py:31, jax.nn.gelu(approximate=False)) in fp64.  CPU only: pins the constants
-and the error bound the kernel's comment states (relative <= 5.7e-6, absolute <= 9.6e-7 on
-[-30, 30]), far below the bf16 output rounding (2^-9)."""
+and the error bound the kernel's comment states (relative <= 2.2e-5 where |gelu| > 1e-6, absolute
+<= 3.0e-6 on [-30, 30]), far below the bf16 output rounding (2^-9)."""
 
 import os
 import re
@@ -35,13 +35,13 @@ def gelu_epilogue_f32(x):
 
 def test_gelu_epilogue_error_bound():
     x = np.concatenate([np.linspace(-30, 30, 600001), np.linspace(-6, 6, 400001),
-                        np.array([0.0, -0.0, 1e-30, -1e-30, 5.6, -5.6, 5.61, -5.61])]).astype(np.float32)
+                        np.array([0.0, -0.0, 1e-30, -1e-30, 5.3, -5.3, 5.31, -5.31])]).astype(np.float32)
     g = gelu_epilogue_f32(x).astype(np.float64)
     ref = x.astype(np.float64) * ndtr(x.astype(np.float64))
     err = np.abs(g - ref)
     m = np.abs(ref) > 1e-6
-    assert err.max() <= 1.0e-6, err.max()
-    assert (err[m] / np.abs(ref[m])).max() <= 6e-6, (err[m] / np.abs(ref[m])).max()
+    assert err.max() <= 3.0e-6, err.max()
+    assert (err[m] / np.abs(ref[m])).max() <= 2.2e-5, (err[m] / np.abs(ref[m])).max()
 
 
 def test_gelu_epilogue_limits():

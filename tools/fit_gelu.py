@@ -62,8 +62,9 @@ def fit_tanh(y0=0.48, deg=3):
     return c, err
 
 
-def fit_log2(deg=7, tmax=5.6):
-    """Production GELU epilogue (gemm_epilogue.h gelu_fast2): P(t) ~ log2 Phi(-t) on [0, tmax],
+def fit_log2(deg=6, tmax=5.3):
+    """Production GELU epilogue (gemm_epilogue.h gelu_fast2, degree 6 on [0, 5.3]; round 2's first
+    form was degree 7 on [0, 5.6]): P(t) ~ log2 Phi(-t) on [0, tmax],
     gelu(x) = max(x, 0) - t * exp2(P(t)), t = min(|x|, tmax).  Returns the coefficients and the
     fp32 relative / absolute error of the whole GELU against x*Phi(x) on [-30, 30]."""
     from scipy.special import log_ndtr, ndtr
@@ -87,9 +88,9 @@ def fit_log2(deg=7, tmax=5.6):
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "log2":
-    for deg in (6, 7, 8):
-        c, rel, ab = fit_log2(deg)
-        print(f"log2 form degree {deg}: rel {rel:.2e} abs {ab:.2e}:", ", ".join(f"{float(np.float32(v))!r}f" for v in c))
+    for deg, tmax in ((6, 5.3), (6, 5.6), (7, 5.6), (8, 5.6)):
+        c, rel, ab = fit_log2(deg, tmax)
+        print(f"log2 form degree {deg} on [0, {tmax}]: rel {rel:.2e} abs {ab:.2e}:", ", ".join(f"{float(np.float32(v))!r}f" for v in c))
 
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "tanh":

@@ -179,6 +179,7 @@ def grouped(dev, g):
         fns = {"grouped": lambda: nat.dev_gemm_ln(a, w, b, epi, o, ln_rs=rs, ln_c=c)}
         if epi == nat.EPI_GELU_LN:
             fns["ungrouped"] = lambda: nat.dev_gemm_ln(a, w, b, 3011, o, ln_rs=rs, ln_c=c)
+            fns["gelu-deg6"] = lambda: nat.dev_gemm_ln(a, w, b, 3012, o, ln_rs=rs, ln_c=c)
         res = {k: [] for k in fns}
         for _ in range(3):
             for k, f in fns.items():

@@ -34,25 +34,25 @@ struct EpiTraits {
 
 // GELU(x) = x * Phi(x) (exact-erf form, layers.py:31) in one transcendental:
 //   gelu(x) = max(x, 0) - t * Phi(-t),   t = min(|x|, GELU_TMAX),
-//   Phi(-t) = exp2(P(t)),  P = degree-7 fit of log2 Phi(-t) on [0, 5.6] (tools/fit_gelu.py log2).
-// fp32 result vs x*Phi(x) in fp64: relative error <= 5.7e-6, absolute <= 9.6e-7 (checked on
-// [-30, 30] with fp32 Horner); beyond |x| = 5.6 the clamped term is below 6e-8.  Per value pair:
-// 2 min, 7 packed FMA, 2 exp2, 2 max, 1 packed FMA = 12 VALU + 2 transcendental issues (the
-// former A&S 7.1.26 form needed 13 + 4: an rcp and an exp2 per value).
-constexpr float GELU_TMAX = 5.6f;
-#define VP_GELU_P7 -1.8099689214068349e-06f
-#define VP_GELU_P6 6.117992597864941e-05f
-#define VP_GELU_P5 -0.0009278103243559599f
-#define VP_GELU_P4 0.00849936343729496f
-#define VP_GELU_P3 -0.05394672974944115f
-#define VP_GELU_P2 -0.45847392082214355f
-#define VP_GELU_P1 -1.1512486934661865f
-#define VP_GELU_P0 -0.9999953508377075f
+//   Phi(-t) = exp2(P(t)),  P = degree-6 fit of log2 Phi(-t) on [0, 5.3] (tools/fit_gelu.py log2).
+// fp32 result vs x*Phi(x) in fp64: relative error <= 2.2e-5 where |gelu| > 1e-6, absolute
+// <= 3.0e-6 (checked on [-30, 30] with fp32 Horner, tests/test_epilogue_math.py): 1 % of the bf16
+// output's half-ulp (2^-9).  Per value pair: 2 min, 6 packed FMA, 2 exp2, 2 max, 1 packed FMA = 11
+// VALU + 2 transcendental issues.  (Degree 7 on [0, 5.6], relative 5.7e-6, took one packed FMA more
+// per pair: ffn_layer1 598.9 -> 588.1 us with degree 6, tools/gemm_bench.py; the A&S 7.1.26 form
+// before it needed 13 + 4 issues.)
+constexpr float GELU_TMAX = 5.3f;
+#define VP_GELU_P6 2.7470525310491212e-05f
+#define VP_GELU_P5 -0.000680534983985126f
+#define VP_GELU_P4 0.007596395444124937f
+#define VP_GELU_P3 -0.05224345251917839f
+#define VP_GELU_P2 -0.46002063155174255f
+#define VP_GELU_P1 -1.1507104635238647f
+#define VP_GELU_P0 -1.0000278949737549f
 
 __device__ __forceinline__ float gelu_fast(float x) {
   const float t = __builtin_fminf(__builtin_fabsf(x), GELU_TMAX);
-  float p = fmaf(t, VP_GELU_P7, VP_GELU_P6);
-  p = fmaf(t, p, VP_GELU_P5);
+  float p = fmaf(t, VP_GELU_P6, VP_GELU_P5);
   p = fmaf(t, p, VP_GELU_P4);
   p = fmaf(t, p, VP_GELU_P3);
   p = fmaf(t, p, VP_GELU_P2);
@@ -66,8 +66,7 @@ __device__ __forceinline__ float gelu_fast(float x) {
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t x) {
   const f32x2_t t = {__builtin_fminf(__builtin_fabsf(x.x), GELU_TMAX), __builtin_fminf(__builtin_fabsf(x.y), GELU_TMAX)};
-  f32x2_t p = __builtin_elementwise_fma(t, f32x2_t(VP_GELU_P7), f32x2_t(VP_GELU_P6));
-  p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P5));
+  f32x2_t p = __builtin_elementwise_fma(t, f32x2_t(VP_GELU_P6), f32x2_t(VP_GELU_P5));
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P4));
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P3));
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P2));
