@@ -190,6 +190,30 @@ def grouped(dev, g):
         del a, o
 
 
+def s3_ab(dev, g):
+    """ffn_layer2 shape: S3 staging (production for K >= 2048: three A buffers, A pieces in h0)
+    vs the PF 2 build it replaced -- plain epilogue, no epilogue, and the production residual +
+    row-statistics epilogue."""
+    M, N, K = M_TOK, 768, 3072
+    a, w, b = operands(M, N, K, g, dev)
+    o = torch.zeros((M, N), device=dev, dtype=torch.bfloat16)
+    part = torch.empty((N // 128, M, 2), device=dev)
+    fns = {"pf2": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 9102, o),
+           "s3": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 9100, o),
+           "noepi-2stage": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 8, o),
+           "noepi-s3": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 9108, o),
+           "st-pf2": lambda: nat.dev_gemm_ln(a, w, b, 10111, o, resid=o, st_part=part),
+           "st-s3 (production)": lambda: nat.dev_gemm_ln(a, w, b, nat.EPI_RESID_FFN_BF16_ST, o, resid=o,
+                                                         st_part=part)}
+    res = {k: [] for k in fns}
+    for _ in range(3):
+        for k, f in fns.items():
+            res[k].append(timeit(f))
+    flop = 2.0 * M * N * K
+    print("ffn2 staging:", " | ".join(f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()),
+          flush=True)
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -200,6 +224,8 @@ def main():
         variants(dev, g, 4, [0, 8, 32, 5000, 5001, 5002, 5003])
     elif mode == "grouped":
         grouped(dev, g)
+    elif mode == "s3":
+        s3_ab(dev, g)
     elif mode == "skew":
         skew(dev, g)
     elif mode == "msize":

@@ -60,10 +60,19 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // unpacked fp32 arithmetic (A/B), 2048 / 4096 = epilogue without the LDS transposition's
 // writes / read-backs.
 // PF > 0: L2 prefetch of A, PF K-tiles beyond the K-tile being staged (one dword per A row per
-// K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  Pays where A streams
-// from HBM (ffn_layer2, K = 3072: 490 -> 471 us); costs on the K = 768 shapes (A mostly from the
-// Infinity Cache).
-template <int EPI, int DIAG = 0, int PF = 0>
+// K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  ffn_layer2, K = 3072:
+// 490 -> 471 us; costs on the K = 768 shapes (A mostly from the Infinity Cache).  Superseded for
+// K >= 2048 by S3 (below; A/B build only).
+// S3 (K >= 2048: ffn_layer2, whose A -- the 805 MB hidden activation -- streams from HBM): three
+// 32 KiB A buffers and two W buffers (all 160 KiB).  A K-tile's A pieces are issued in the h0 of
+// the K-tile two before it (into the A buffer freed by the K-tile before that), its W pieces in
+// the h1, so A gets 1.5 K-tiles of lead and the 16 pieces are spread over both phases.  The
+// epilogue's scratch is the A buffer of the tile's last K-tile, refilled by the next h0.
+// Bitwise equal to the 2-stage kernel; ffn_layer2 (statistics epilogue) 501.8 -> 485.6 us isolated,
+// 7.78 -> 7.48 ms/step in the forward (tools/gemm_bench.py s3).  (Three A stages with all 16
+// pieces in h1 measured 468 vs 475 us isolated and nothing in the forward; the lead time alone is
+// not it -- spreading the pieces over both phases is.)
+template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, int ngrp, EpiArgs ep) {
@@ -137,9 +146,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       coords(ld_tile, ld_tm, ld_tn);
     }
   };
-  auto stage_piece = [&](int buf, int p) {  // p: 0..7 A pieces, 8..15 W pieces
+  // LDS: 2 x [A | W] K-tile buffers; S3: A buffers 0..2 then W buffers 0..1
+  auto a_buf = [&](int ai) { return smem + ai * (S3 ? kOp : kBuf); };
+  auto w_buf = [&](int wi) { return smem + (S3 ? 3 * kOp + wi * kOp : wi * kBuf + kOp); };
+  // p: 0..7 A pieces into A buffer `buf`, 8..15 W pieces into W buffer `buf`
+  auto stage_piece = [&](int buf, int p) {
     const int i = p & 7;
-    char* dst = smem + buf * kBuf + (p >= 8 ? kOp : 0) + (w * 8 + i) * 1024;
+    char* dst = (p >= 8 ? w_buf(buf) : a_buf(buf)) + (w * 8 + i) * 1024;
     if (p < 8) {
       const uint32_t so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
@@ -156,17 +169,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   for (int kh = 0; kh < 2; ++kh) {
     const int ch = ((kh * 4 + (lane >> 4)) ^ swz(frow)) * 16;
     aoff[kh] = (wm * 128 + frow) * 128 + ch;
-    woff[kh] = kOp + (wn * 128 + frow) * 128 + ch;
+    woff[kh] = (wn * 128 + frow) * 128 + ch;
   }
   bf16x8 fa[2][8], fw[2][8];
-  auto rd = [&](int set, int buf, int q) {  // fragment q of A (q < 8) or W, k-half `set`
+  // fragment q of A (q < 8, A buffer ab) or W (W buffer wb), k-half `set`
+  auto rd = [&](int set, int ab, int wb, int q) {
     if constexpr (DIAG & 2) {
       asm volatile("" : "+v"(fa[set][q & 7]), "+v"(fw[set][q & 7]));
       return;
     }
-    const char* base = smem + buf * kBuf;
-    if (q < 8) fa[set][q] = *reinterpret_cast<const bf16x8*>(base + aoff[set] + q * 2048);
-    else fw[set][q - 8] = *reinterpret_cast<const bf16x8*>(base + woff[set] + (q - 8) * 2048);
+    if (q < 8) fa[set][q] = *reinterpret_cast<const bf16x8*>(a_buf(ab) + aoff[set] + q * 2048);
+    else fw[set][q - 8] = *reinterpret_cast<const bf16x8*>(w_buf(wb) + woff[set] + (q - 8) * 2048);
   };
 
   f32x4 acc[8][8];
@@ -189,20 +202,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   __builtin_amdgcn_s_barrier();
   sched_fence();
 #pragma unroll
-  for (int q = 0; q < 16; ++q) rd(0, 0, q);
+  for (int q = 0; q < 16; ++q) rd(0, 0, 0, q);
+  int a3 = 0;  // S3: A buffer of the K-tile being computed (g % 3)
 
   uint32_t pf_dummy = 0;  // PF: destination of the L2-prefetch loads (never read)
   auto h0 = [&](int cb, bool zero) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     sched_fence();
+    const int a_ld = a3 == 0 ? 2 : a3 - 1;  // S3: A buffer of K-tile g+2 (freed by K-tile g-1)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) rd(1, cb, q);
+    for (int q = 0; q < 16; ++q) {
+      rd(1, S3 ? a3 : cb, cb, q);
+      if constexpr (S3) {
+        if (q < 8) stage_piece(a_ld, q);
+      }
+    }
 #pragma unroll
     for (int idx = 0; idx < 64; ++idx) mfma(0, idx, zero);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if constexpr (S3) {
+        if (q < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     }
     sched_fence();
@@ -214,7 +237,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // drain behind the next tile's MFMAs
   auto h1 = [&](int cb, bool after_epi) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (after_epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    // S3: K-tile g+1 has landed once all but this K-tile's h0 A pieces (of g+2) are done
+    if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (after_epi) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     else if constexpr (PF > 0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sched_fence();
@@ -223,10 +248,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     sched_fence();
     __builtin_amdgcn_s_barrier();
     sched_fence();
+    const int an = a3 == 2 ? 0 : a3 + 1;  // S3: A buffer of K-tile g+1
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      rd(0, cb ^ 1, q);
-      if constexpr (!(DIAG & 4)) stage_piece(cb, q);
+      rd(0, S3 ? an : (cb ^ 1), cb ^ 1, q);
+      if constexpr (S3) {
+        if (q >= 8) stage_piece(cb, q);  // W of K-tile g+2 into W buffer cb
+      } else if constexpr (!(DIAG & 4)) {
+        stage_piece(cb, q);
+      }
     }
 #pragma unroll
     for (int idx = 2; idx < 64; ++idx) mfma(1, idx, false);
@@ -260,6 +290,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "+v"(pf_dummy) : "v"(voff), "s"(rsA));
       sched_fence();
     }
+    if constexpr (S3) a3 = an;
     advance();  // after the scheduled block: its branch must not split it
   };
 
@@ -322,7 +353,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     coords(first + j * stride, etm, etn);
     const int m0 = etm * BM + wm * 128, n0 = etn * BN + wn * 128;
     using Tr = EpiTraits<EPI>;
-    char* scr = smem + kLds + w * kScr;
+    // S3: the A buffer of the tile's last K-tile (free since its h1 barrier; refilled in the next h0)
+    char* scr = (S3 ? a_buf(a3 == 0 ? 2 : a3 - 1) : smem + kLds) + w * kScr;
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)
     F8 ex[2][2][2];  // [buffer][nh][pass]
@@ -442,7 +474,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-constexpr int kPfLongK = 2;  // A prefetch distance (K-tiles) for K >= 2048
+[[maybe_unused]] constexpr int kPfLongK = 2;  // A prefetch distance (K-tiles) of the PF build (A/B; K >= 2048 uses S3)
 
 int num_cus_w4() {
   static int n = 0;
@@ -467,12 +499,12 @@ int w4_ngrp(int M, int N, int K, int grid) {
   return g;
 }
 
-template <int EPI, int DIAG = 0, int PF = 0>
+template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG, PF>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -480,8 +512,8 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
   const int ngrp = (DIAG & 32768) ? N / BN : w4_ngrp(M, N, K, grid);  // DIAG 32768: ungrouped (A/B)
-  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF>));
-  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
+  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>));
+  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
                      ldw, M, N, K, ngrp, ep);
   return hipGetLastError();
 }
@@ -502,13 +534,13 @@ hipError_t w4_dispatch_d(int epi, const bf16_t* A, int64_t lda, const bf16_t* W,
     case EPI_RESID_BF16: return launch_w4<EPI_RESID_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16: return launch_w4<EPI_POS_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN_BF16:
-      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16, D, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_RESID_FFN_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_BF16_LN: return launch_w4<EPI_BF16_LN, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_GELU_BF16_LN: return launch_w4<EPI_GELU_BF16_LN, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN_BF16_ST:
-      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, D, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_RESID_FFN_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RELU_BF16: return launch_w4<EPI_RELU_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
@@ -554,6 +586,12 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 5001: return launch_w4<EPI_BF16, 4096>(A, lda, W, ldw, M, N, K, ep, s);
       case 5002: return launch_w4<EPI_BF16, 6144>(A, lda, W, ldw, M, N, K, ep, s);
       case 5003: return launch_w4<EPI_BF16, 6144 | 32>(A, lda, W, ldw, M, N, K, ep, s);
+      // S3 staging (production for K >= 2048) with the plain epilogue / without epilogue, and the
+      // former K >= 2048 production (PF 2) with the statistics epilogue, for A/B
+      case 9100: return launch_w4<EPI_BF16, 0, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
+      case 9108: return launch_w4<EPI_BF16, 8, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
+      case 9102: return launch_w4<EPI_BF16, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
+      case 9111: return launch_w4<EPI_RESID_FFN_BF16_ST, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
       // the ffn_layer1 production epilogue without the N-tile grouping (A/B of w4_ngrp)
       case 2011: return launch_w4<EPI_GELU_BF16_LN, 512 | 32768>(A, lda, W, ldw, M, N, K, ep, s);
       case 1024: return launch_w4<EPI_BF16, 0, 2>(A, lda, W, ldw, M, N, K, ep, s);
