@@ -63,7 +63,8 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // K-tile, the youngest VMEM op of an h1, so the next h1 waits vmcnt(1)).  ffn_layer2, K = 3072:
 // 490 -> 471 us; costs on the K = 768 shapes (A mostly from the Infinity Cache).  Superseded for
 // K >= 2048 by S3 (below; A/B build only).
-// S3 (K >= 2048: ffn_layer2, whose A -- the 805 MB hidden activation -- streams from HBM): three
+// S3 (ffn_layer2, whose A -- the 805 MB hidden activation -- streams from HBM; also the q|k|v and
+// post projections, whose A the previous kernel wrote with nontemporal stores): three
 // 32 KiB A buffers and two W buffers (all 160 KiB).  A K-tile's A pieces are issued in the h0 of
 // the K-tile two before it (into the A buffer freed by the K-tile before that), its W pieces in
 // the h1, so A gets 1.5 K-tiles of lead and the 16 pieces are spread over both phases.  The
@@ -536,9 +537,11 @@ hipError_t w4_dispatch_d(int epi, const bf16_t* A, int64_t lda, const bf16_t* W,
     case EPI_RESID_FFN_BF16:
       if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_RESID_FFN_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_BF16_LN: return launch_w4<EPI_BF16_LN, D>(A, lda, W, ldw, M, N, K, ep, s);
+    // q|k|v projection and post projection: S3 staging (forward, one box, alternating runs: qkv
+    // 6.74-6.76 -> 6.50-6.54 ms/step, post 2.82-2.83 -> 2.69-2.71); ffn_layer1 measured no gain
+    case EPI_BF16_LN: return launch_w4<EPI_BF16_LN, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_GELU_BF16_LN: return launch_w4<EPI_GELU_BF16_LN, D>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN_BF16_ST:
       if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_RESID_FFN_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
