@@ -13,10 +13,12 @@ def w4_ngrp(M, N, K, grid):
     """gemm_bf16_w4.hip w4_ngrp: N-tile group size of the grouped tile order."""
     tiles_n = N // BN
     w_tile = BN * K * 2
-    if tiles_n * w_tile <= (4 << 20) or K >= 2048 or (M // BM) % 8 or grid % 8:
+    w_all = tiles_n * w_tile
+    if w_all <= (2 << 20) or K >= 2048 or (M // BM) % 8 or grid % 8:
         return tiles_n
+    budget = (5 << 19) if w_all > (4 << 20) else w_all // 2
     for d in range(tiles_n, 0, -1):
-        if tiles_n % d == 0 and d * w_tile <= (5 << 19):
+        if tiles_n % d == 0 and d * w_tile <= budget:
             return d
     return tiles_n
 
@@ -66,15 +68,16 @@ def test_every_tile_once(clips, N, K):
     assert len(seen) == len(set(seen)) == (M // BM) * (N // BN)
     assert all(0 <= tm < M // BM and 0 <= tn < N // BN for tm, tn in seen)
     if ngrp < N // BN:  # grouped: the group's W rows fit the 2.5 MB budget, A is not HBM-streamed
-        assert ngrp * BN * K * 2 <= (5 << 19) and K < 2048
+        assert ngrp * BN * K * 2 <= (5 << 19) and K < 2048 and (N // BN) * BN * K * 2 > (2 << 20)
 
 
 def test_grouping_applies_where_intended():
-    # Base ffn_layer1 at B = 32: W = 4.7 MB > an XCD's L2 -> groups of 6 N-tiles;
-    # Base qkv (3.5 MB) and ffn_layer2 (K = 3072, A from HBM) stay ungrouped; Large ffn1 / qkv: 4
+    # Base ffn_layer1 at B = 32: W = 4.7 MB > an XCD's L2 -> groups of 6 N-tiles; Base qkv (3.5 MB)
+    # groups of 3; ffn_layer2 (K = 3072, A from HBM) and post (1.2 MB) stay ungrouped; Large ffn1 / qkv: 4
     M = 32 * 16 * 256
     assert schedule(M, 3072, 768)[1] == 6
-    assert schedule(M, 2304, 768)[1] == 9
+    assert schedule(M, 2304, 768)[1] == 3
+    assert schedule(M, 768, 768)[1] == 3
     assert schedule(M, 768, 3072)[1] == 3
     assert schedule(16 * 16 * 256, 4096, 1024)[1] == 4
     assert schedule(16 * 16 * 256, 3072, 1024)[1] == 4
