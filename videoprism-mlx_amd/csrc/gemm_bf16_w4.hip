@@ -23,6 +23,12 @@
 //    one M row (8-byte bf16 / 16-byte fp32 stores), as in gemm_bf16.hip.
 //  * The K-tile stream runs across the persistent workgroup's tiles: the next tile's first
 //    K-tiles load during this tile's last K-tiles and epilogue.
+//  * S3 variant (q|k|v, post and ffn_layer2 in the forward): a third A buffer lets each
+//    K-tile's A pieces go out in the h0 of the K-tile two before it (W pieces stay in h1), so the
+//    A stream the previous kernel just wrote gets 1.5 K-tiles of lead and the VMEM issue is spread
+//    over both phases; the epilogue's scratch lives in the A buffer its last K-tile freed.
+//  * Tile order: XCD-contiguous tile ranges; where W outgrows the XCD's L2 share the XCD sweeps
+//    its M-blocks once per group of N-tiles (w4_ngrp), so a group's W stays L2-resident.
 #include <cstdlib>
 
 #include "gemm_epilogue.h"
