@@ -82,25 +82,35 @@ WORKLOADS = {
 }
 
 
-def cpu_baseline(cfg, variables) -> dict:
-    """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip — a reported baseline only.  BLAS
-    threads pinned to CPU_BASELINE_THREADS (the box's CPU share per GPU)."""
+def cpu_baseline(cfg, variables, runs: int = 3) -> dict:
+    """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip -- a reported baseline only.  BLAS
+    threads pinned to CPU_BASELINE_THREADS (the box's CPU share per GPU); one untimed warm-up
+    run, then `runs` timed runs: value = 1 / mean, with mean +- std in the sample text
+    (SURVEY §8(d) method, scaled to the bench's time budget)."""
     import numpy as np
     from threadpoolctl import threadpool_info, threadpool_limits
 
     from oracle import videoprism_oracle as orc
     rng = np.random.default_rng(0)
     video = rng.random((1, 16, 288, 288, 3), dtype=np.float32)
+    times = []
     with threadpool_limits(limits=CPU_BASELINE_THREADS):
         threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-        t0 = time.perf_counter()
-        orc.factorized_encoder(variables["params"], video, cfg, mode="f32")
-        dt = time.perf_counter() - t0
-    return {"value": round(1.0 / dt, 5), "unit": "clips/s", "cores": int(threads), "kind": "port",
+        for i in range(runs + 1):
+            t0 = time.perf_counter()
+            orc.factorized_encoder(variables["params"], video, cfg, mode="f32")
+            if i > 0:
+                times.append(time.perf_counter() - t0)
+    mean, std = float(np.mean(times)), float(np.std(times))
+    return {"value": round(1.0 / mean, 5), "unit": "clips/s", "cores": int(threads), "kind": "port",
             "sample": f"1 clip [1,16,288,288,3], full {cfg.get('_name', 'model')} forward, NumPy fp32 "
-                      f"oracle (oracle/videoprism_oracle.py), {dt:.1f} s with BLAS pinned to "
-                      f"{threads} threads; the host exposes {len(os.sched_getaffinity(0))} "
-                      f"schedulable CPUs"}
+                      f"oracle (oracle/videoprism_oracle.py): 1 warm-up + {runs} timed runs, "
+                      f"{mean:.2f} +- {std:.2f} s per clip (min {min(times):.2f}, max {max(times):.2f}) "
+                      f"with BLAS pinned to {threads} threads; the host exposes "
+                      f"{len(os.sched_getaffinity(0))} schedulable CPUs.  For context, the reference's "
+                      f"published Flax-on-CPU time is 4.54 s per LvT-B pass on an Apple M3 Pro "
+                      f"(FLAX_TO_MLX_CONVERSION_GUIDE.md:408); JAX cannot run here",
+            "runs_s": [round(t, 3) for t in times]}
 
 
 def load_traffic(path: str, symbol: str, workload: str, src_hash: str):
@@ -127,18 +137,44 @@ def _free_port() -> int:
     return p
 
 
-def spawn_ranks(n: int) -> int:
+def spawn_ranks(n: int, timeout_s: float) -> int:
     """--gpus N without a launcher: N child processes of this script (RANK/LOCAL_RANK/WORLD_SIZE/
-    MASTER_ADDR/MASTER_PORT set), started before this parent touches any GPU.  Returns the first
-    non-zero exit code (0 if all ranks succeeded)."""
+    MASTER_ADDR/MASTER_PORT set), started before this parent touches any GPU.  All children are
+    polled: the first non-zero exit (a rank that died, e.g. before the rendezvous, would leave its
+    siblings blocked in it) or the overall timeout terminates the others (exact PIDs), and that
+    code -- 124 for the timeout -- is returned; 0 when every rank succeeded."""
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    return next((c for c in codes if c != 0), 0)
+    deadline = time.monotonic() + timeout_s
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = next((c for c in codes if c not in (None, 0)), None)
+        if bad is not None:
+            rc = bad
+            print(f"bench: a rank exited with {bad}; stopping the others", file=sys.stderr)
+            break
+        if all(c == 0 for c in codes):
+            return 0
+        if time.monotonic() > deadline:
+            rc = 124
+            print(f"bench: ranks still running after {timeout_s:.0f} s; stopping them", file=sys.stderr)
+            break
+        time.sleep(0.2)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=15)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc if rc > 0 else 1
 
 
 # ------------------------------------------------------------------------------------------
@@ -215,16 +251,27 @@ def main() -> None:
                     help="PMC traffic record (default profiles/traffic_r02_<workload>.json)")
     ap.add_argument("--standin", action="store_true",
                     help="CPU stand-in forward over gloo: multi-process plumbing test, no measurement")
+    ap.add_argument("--spawn-timeout", type=float, default=1200.0,
+                    help="seconds before self-spawned ranks are stopped (--gpus N without a launcher)")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # launcher tests
+    ap.add_argument("--hang-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, args.spawn_timeout))
+    if args.fail_rank >= 0 and int(os.environ.get("RANK", 0)) == args.fail_rank:
+        sys.exit(3)  # a rank that dies before the rendezvous (tests/test_distributed_cpu.py)
+    if args.hang_rank >= 0 and int(os.environ.get("RANK", 0)) == args.hang_rank:
+        time.sleep(3600)  # a rank that never joins (same tests)
 
     import torch
 
     from videoprism import _native, distributed, models, params
 
-    rank, local_rank, world = distributed.init("gloo" if args.standin else "nccl")
+    # the process group is CPU-side (gloo) on GPU ranks too: it carries only the rendezvous, the
+    # RCCL id broadcast, the barrier and the max-over-ranks; the library's vp_comm is each rank's
+    # only RCCL communicator
+    rank, local_rank, world = distributed.init("gloo")
     if world != args.gpus:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
@@ -270,7 +317,7 @@ def main() -> None:
         def step():
             vemb = ops.encode_video(video)
             if gather:
-                vemb = distributed.all_gather_rows(vemb, world, comm)
+                vemb = distributed.all_gather_rows(vemb, world, comm, counts=[B] * world)
             temb = ops.encode_text(ids, tpad)
             last["rows"], last["sim"] = vemb, ops.similarity(vemb, temb)
     else:
@@ -280,7 +327,8 @@ def main() -> None:
         def step():
             ops.forward(video, out)
             if gather:
-                last["rows"] = distributed.all_gather_rows(ops.pool_l2(out), world, comm)
+                last["rows"] = distributed.all_gather_rows(ops.pool_l2(out), world, comm,
+                                                           counts=[B] * world)
 
     sync = (lambda: None) if args.standin else torch.cuda.synchronize
     for _ in range(args.warmup):
@@ -303,14 +351,14 @@ def main() -> None:
         dom_symbol = eng.kernel_name(dom_name)
         eng.profile_only([dom_name])
         eng.profile_enable(args.steps * launches_per_fwd + 16)
-    distributed.barrier(None if args.standin else dev)
+    distributed.barrier()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     sync()
-    distributed.barrier(None if args.standin else dev)
-    elapsed = distributed.max_over_ranks(time.perf_counter() - t0, None if args.standin else dev)
+    distributed.barrier()
+    elapsed = distributed.max_over_ranks(time.perf_counter() - t0)
     prof = eng.profile_read() if profile else {}
     if profile:
         eng.profile_enable(0)

@@ -143,7 +143,9 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
 /* Capped attention over rows qkv[num_seq*S, 3*heads*64] = [q|k|v] (q pre-scaled), writing
  * o[num_seq*S, heads*64].  Replaces DotProductAttention._dot_atten (layers.py:601-661).
  * precision VP_BF16 (S == 256 or S <= 16; S a multiple of 256 without key_pad: the long-sequence
- * kernel of the LvT auxiliary encoder) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL. */
+ * kernel of the LvT auxiliary encoder) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL.
+ * bf16 with a cap outside (0, 50] (no capping, or one whose unnormalised fp32 numerators could
+ * overflow) runs the online-softmax kernel of vp_op_attention_masked, any S. */
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
                     int64_t heads, float cap, const float* key_pad, void* stream);
 
@@ -262,7 +264,10 @@ int vp_classifier_forward(vp_classifier* c, const void* video, int in_dtype, int
  * every rank by any channel (videoprism/distributed.py uses torch.distributed), and every rank
  * calls vp_comm_init with it (collective: blocks until all nranks joined).
  * vp_allgather: recv[r*count .. (r+1)*count) = rank r's send[0 .. count) on every rank, dtype
- * VP_F32 / VP_BF16 / VP_U8, asynchronous on `stream` (device pointers of the comm's device). */
+ * VP_F32 / VP_BF16 / VP_U8, asynchronous on `stream` (device pointers of the comm's device).
+ * `count` must be the same on every rank (RCCL's contract): hosts with uneven shards pad to the
+ * largest (videoprism/distributed.py Communicator.all_gather_rows).  Every vp_comm_* entry point
+ * leaves the calling thread's current HIP device as it found it. */
 typedef struct vp_comm vp_comm;
 int vp_comm_id_bytes(void);
 int vp_comm_unique_id(uint8_t* id_out, int64_t nbytes);

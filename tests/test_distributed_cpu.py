@@ -29,8 +29,15 @@ def _worker(rank, world, port, q):
     local = torch.arange(lo, hi, dtype=torch.float32)[:, None].repeat(1, 3)
     gathered = distributed.all_gather_rows(local, w)
     t = distributed.max_over_ranks(float(rank + 1))
+    # uneven and empty shards (global batch 3 / 1 over 2 ranks): padded to the largest shard for
+    # the collective, padding rows dropped, rank-major order kept
+    uneven = {}
+    for B in (3, 1):
+        ulo, uhi = distributed.shard_range(B, r, w)
+        u = torch.arange(ulo, uhi, dtype=torch.float32)[:, None].repeat(1, 5)
+        uneven[B] = distributed.all_gather_rows(u, w)[:, 0].tolist()
     distributed.barrier()
-    q.put((rank, lo, hi, gathered[:, 0].tolist(), t))
+    q.put((rank, lo, hi, gathered[:, 0].tolist(), t, uneven))
     dist.destroy_process_group()
 
 
@@ -56,10 +63,16 @@ def test_gloo_world2_gather_and_timing():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    for rank, lo, hi, rows, t in res:
+    for rank, lo, hi, rows, t, uneven in res:
         assert rows == [float(i) for i in range(64)]   # every rank sees all clips in order
         assert t == 2.0                                  # max over ranks
-    assert [(lo, hi) for _, lo, hi, _, _ in res] == [(0, 32), (32, 64)]
+        assert uneven == {3: [0.0, 1.0, 2.0], 1: [0.0]}
+    assert [(lo, hi) for _, lo, hi, _, _, _ in res] == [(0, 32), (32, 64)]
+
+
+def _bench_env():
+    return {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
+                                                             "MASTER_ADDR", "MASTER_PORT")}
 
 
 def _bench_standin(workload, batch):
@@ -67,8 +80,7 @@ def _bench_standin(workload, batch):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
-                                                            "MASTER_ADDR", "MASTER_PORT")}
+    env = _bench_env()
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--standin",
                         "--workload", workload, "--batch", str(batch), "--frames", "2", "--steps", "2",
                         "--warmup", "1"], capture_output=True, text=True, timeout=150, env=env)
@@ -97,3 +109,37 @@ def test_bench_spawns_world2_lvt_similarity():
     chk = line["standin_check"]
     assert chk["gathered_shape"] == [6, 768] and chk["row_order_ok"]
     assert chk["similarity_shape"] == [6, 8]
+
+
+@pytest.mark.timeout(200)
+def test_bench_spawn_stops_siblings_of_a_dead_rank():
+    """A rank that dies before the rendezvous (here: rank 1 exits with 3 right after start-up)
+    must not leave rank 0 blocked in init_process_group and the parent in wait(): the parent
+    polls every child, stops the survivor and returns the failing code well inside the timeout."""
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--standin",
+                        "--batch", "2", "--frames", "2", "--steps", "1", "--warmup", "0",
+                        "--fail-rank", "1", "--spawn-timeout", "90"],
+                       capture_output=True, text=True, timeout=150, env=_bench_env())
+    dt = time.monotonic() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert dt < 60, dt
+    assert "stopping the others" in r.stderr
+
+
+@pytest.mark.timeout(200)
+def test_bench_spawn_timeout():
+    """The overall timeout ends a spawned run that does not finish (both ranks alive, rank 1
+    never joins: it sleeps past the timeout) with code 124, both ranks stopped."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--standin",
+                        "--batch", "2", "--frames", "2", "--steps", "1", "--warmup", "0",
+                        "--hang-rank", "1", "--spawn-timeout", "8"],
+                       capture_output=True, text=True, timeout=150, env=_bench_env())
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])

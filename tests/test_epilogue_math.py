@@ -22,7 +22,8 @@ def _coeffs():
 
 
 def gelu_epilogue_f32(x):
-    """The kernel's operation sequence in fp32: t = min(|x|, TMAX); Horner; exp2; fma."""
+    """The kernel's operation sequence in fp32: t = minimum(|x|, TMAX); Horner; exp2; fma (NumPy's
+    minimum / maximum propagate NaN like the kernel's v_minimum3_f32 / v_maximum3_f32)."""
     c, tmax = _coeffs()
     x = np.asarray(x, np.float32)
     t = np.minimum(np.abs(x), tmax)
@@ -49,3 +50,15 @@ def test_gelu_epilogue_limits():
     assert g[0] == np.inf and g[2] == np.float32(1e30) and g[4] == np.float32(40.0)
     assert abs(g[1]) < 1e-6
     assert abs(g[3]) < 1e-6 and abs(g[5]) < 1e-6
+
+
+def test_gelu_epilogue_nan_propagates():
+    """A NaN pre-activation (upstream overflow) must come out NaN, as x * Phi(x) does in the
+    reference, not as a small finite value (IEEE minNum / maxNum would absorb it)."""
+    with np.errstate(invalid="ignore"):
+        g = gelu_epilogue_f32(np.array([np.nan, -np.nan], np.float32))
+    assert np.isnan(g).all()
+    src = open(HDR).read()
+    body = src[src.index("gelu_fast2(f32x2_t x)"):src.index("gelu_as2")]
+    assert "__builtin_fminf" not in body and "__builtin_fmaxf" not in body
+    assert body.count("__builtin_elementwise_minimum") == 2 and body.count("__builtin_elementwise_maximum") == 2

@@ -247,6 +247,27 @@ def test_attention_bf16(cuda, S, num_seq, heads, scale):
     assert err.mean() < 2e-3, err.mean()
 
 
+@pytest.mark.parametrize("S,num_seq,heads,cap", [(256, 2, 12, 80.0), (4096, 1, 2, 80.0),
+                                                 (256, 2, 12, 50.0), (4096, 1, 2, 50.0)])
+def test_attention_bf16_saturated_logits_large_v(cuda, S, num_seq, heads, cap):
+    """Saturated logits (|q.k| >> cap, so cap*tanh(.) sits at +-cap) with |v| ~ 200: the max-free
+    kernels' unnormalised fp32 O = sum exp(l) v would overflow for cap = 80 (e^80 * S * |v| >
+    FLT_MAX), so caps above 50 must take the online-softmax kernel; at cap = 50 the fast kernels
+    stay finite.  Both against the fp64 oracle."""
+    qkv = _qkv(num_seq, S, heads, 4242 + S, 40.0)
+    qkv[:, 2 * heads * 64:] *= 200.0
+    qkv = _bf(qkv).to(cuda)
+    out = nat.op_attention(qkv, num_seq, S, heads, cap)
+    torch.cuda.synchronize()
+    o = out.double().cpu().numpy()
+    assert np.isfinite(o).all()
+    ref = _oracle_attention(qkv, num_seq, S, heads, cap)
+    vmax = float(qkv[:, 2 * heads * 64:].float().abs().max())
+    err = np.abs(o - ref)
+    print(f"cap {cap} S {S}: max-abs {err.max():.3e} (max|v| {vmax:.0f})")
+    assert np.all(err <= 2 ** -8 * (np.abs(ref) + vmax)), err.max()
+
+
 @pytest.mark.parametrize("S,num_seq", [(256, 3), (16, 10), (8, 6)])
 def test_attention_bf16_key_padding(cuda, S, num_seq):
     heads = 12

@@ -41,6 +41,9 @@ struct EpiTraits {
 // VALU + 2 transcendental issues.  (Degree 7 on [0, 5.6], relative 5.7e-6, took one packed FMA more
 // per pair: ffn_layer1 598.9 -> 588.1 us with degree 6, tools/gemm_bench.py; the A&S 7.1.26 form
 // before it needed 13 + 4 issues.)
+// The clamp and max(x, 0) are IEEE-754-2019 minimum / maximum (gfx950 v_minimum3_f32 /
+// v_maximum3_f32, same issue cost as v_min / v_max): a NaN pre-activation stays NaN, as in the
+// reference's x * Phi(x), instead of being absorbed by minNum / maxNum; +inf gives +inf.
 constexpr float GELU_TMAX = 5.3f;
 #define VP_GELU_P6 2.7470525310491212e-05f
 #define VP_GELU_P5 -0.000680534983985126f
@@ -51,21 +54,22 @@ constexpr float GELU_TMAX = 5.3f;
 #define VP_GELU_P0 -1.0000278949737549f
 
 __device__ __forceinline__ float gelu_fast(float x) {
-  const float t = __builtin_fminf(__builtin_fabsf(x), GELU_TMAX);
+  const float t = __builtin_elementwise_minimum(__builtin_fabsf(x), GELU_TMAX);
   float p = fmaf(t, VP_GELU_P6, VP_GELU_P5);
   p = fmaf(t, p, VP_GELU_P4);
   p = fmaf(t, p, VP_GELU_P3);
   p = fmaf(t, p, VP_GELU_P2);
   p = fmaf(t, p, VP_GELU_P1);
   p = fmaf(t, p, VP_GELU_P0);
-  return fmaf(-t, __builtin_amdgcn_exp2f(p), __builtin_fmaxf(x, 0.0f));
+  return fmaf(-t, __builtin_amdgcn_exp2f(p), __builtin_elementwise_maximum(x, 0.0f));
 }
 
 // The same operation sequence on two values with packed fp32 math (v_pk_fma_f32):
 // bit-identical to two gelu_fast calls, fewer VALU issue slots.
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t x) {
-  const f32x2_t t = {__builtin_fminf(__builtin_fabsf(x.x), GELU_TMAX), __builtin_fminf(__builtin_fabsf(x.y), GELU_TMAX)};
+  const f32x2_t t = {__builtin_elementwise_minimum(__builtin_fabsf(x.x), GELU_TMAX),
+                     __builtin_elementwise_minimum(__builtin_fabsf(x.y), GELU_TMAX)};
   f32x2_t p = __builtin_elementwise_fma(t, f32x2_t(VP_GELU_P6), f32x2_t(VP_GELU_P5));
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P4));
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P3));
@@ -73,7 +77,7 @@ __device__ __forceinline__ f32x2_t gelu_fast2(f32x2_t x) {
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P1));
   p = __builtin_elementwise_fma(t, p, f32x2_t(VP_GELU_P0));
   const f32x2_t e = {__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
-  const f32x2_t m = {__builtin_fmaxf(x.x, 0.0f), __builtin_fmaxf(x.y, 0.0f)};
+  const f32x2_t m = {__builtin_elementwise_maximum(x.x, 0.0f), __builtin_elementwise_maximum(x.y, 0.0f)};
   return __builtin_elementwise_fma(-t, e, m);
 }
 
@@ -127,7 +131,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& ep, int row, int n, flo
                                           float4 extra) {
   using Tr = EpiTraits<EPI>;
   if constexpr (Tr::kGelu) v = gelu4(v);
-  if constexpr (Tr::kRelu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+  if constexpr (Tr::kRelu) v = make_float4(relu_nan(v.x), relu_nan(v.y), relu_nan(v.z), relu_nan(v.w));
   if constexpr (Tr::kKeep) {
     v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep;
   }
@@ -177,7 +181,7 @@ __device__ __forceinline__ float4 epi_math4(float4 v, float keep, float4 extra, 
   } else if (gelu) {
     v = gelu4(v);
   }
-  if (relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+  if (relu) v = make_float4(relu_nan(v.x), relu_nan(v.y), relu_nan(v.z), relu_nan(v.w));
   if (kp) { v.x *= keep; v.y *= keep; v.z *= keep; v.w *= keep; }
   if (ex) { v.x += extra.x; v.y += extra.y; v.z += extra.z; v.w += extra.w; }
   return v;

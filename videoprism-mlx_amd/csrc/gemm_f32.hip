@@ -26,7 +26,7 @@ __device__ __forceinline__ void epi_f32(const EpiArgs& ep, int N, int m, int n, 
     if constexpr (EPI == EPI_GELU_BF16) {
       v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
     } else {
-      v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      v0 = relu_nan(v0); v1 = relu_nan(v1); v2 = relu_nan(v2); v3 = relu_nan(v3);
     }
     if (ep.rowpad) {
       const float keep = 1.0f - ep.rowpad[m];

@@ -559,10 +559,10 @@ int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, in
   if (!qkv || !o || num_seq < 1 || heads < 1) return fail(VP_EINVAL, "bad argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (precision == VP_BF16) {
-    if (!fast_cap(cap))
-      return fail(VP_ENOTSUP, "bf16 vp_op_attention requires 0 < cap <= 80 (max-free softmax); "
-                              "use vp_op_attention_masked for other caps");
-    if (S == 256)
+    if (!fast_cap(cap)) {  // the max-free kernels need 0 < cap <= kMaxFastCap: online softmax
+      if (S < 1) return fail(VP_EINVAL, "bad S");
+      VP_HIP(attention_masked(qkv, o, 1, (int)num_seq, (int)S, (int)heads, cap, key_pad, 0, s));
+    } else if (S == 256)
       VP_HIP(attention_spatial_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)heads, cap, key_pad, s));
     else if (S > 256 && S % 256 == 0 && !key_pad)
       VP_HIP(attention_long_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s));

@@ -28,6 +28,18 @@ int nccl_fail(ncclResult_t r, const char* what) {
   return fail(VP_ECOMM, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+// the calling thread's current HIP device is restored when an entry point returns (the caller
+// may drive another GPU from the same thread)
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -47,6 +59,7 @@ int vp_comm_init(const uint8_t* id, int64_t nbytes, int nranks, int rank, int de
   if (!id || !out || nbytes < (int64_t)sizeof(ncclUniqueId)) return fail(VP_EINVAL, "null argument / short id");
   *out = nullptr;
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(VP_EINVAL, "rank out of range");
+  DeviceGuard guard;
   VP_HIP(hipSetDevice(device));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
@@ -65,7 +78,8 @@ int vp_comm_init(const uint8_t* id, int64_t nbytes, int nranks, int rank, int de
 
 int vp_comm_destroy(vp_comm* c) {
   if (!c) return VP_OK;
-  hipSetDevice(c->device);
+  DeviceGuard guard;
+  (void)hipSetDevice(c->device);
   const ncclResult_t r = c->comm ? ncclCommDestroy(c->comm) : ncclSuccess;
   delete c;
   return r == ncclSuccess ? VP_OK : nccl_fail(r, "ncclCommDestroy");
@@ -80,6 +94,7 @@ int vp_allgather(vp_comm* c, const void* send, void* recv, int64_t count, int dt
     case VP_U8: t = ncclUint8; break;
     default: return fail(VP_EINVAL, "bad dtype");
   }
+  DeviceGuard guard;
   VP_HIP(hipSetDevice(c->device));
   const ncclResult_t r = ncclAllGather(send, recv, (size_t)count, t, c->comm, static_cast<hipStream_t>(stream));
   if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");

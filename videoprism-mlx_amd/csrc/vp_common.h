@@ -106,4 +106,8 @@ __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1
 
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// ReLU that keeps a NaN a NaN like jax.nn.relu (text tower ffn_layer1, encoders.py:743): IEEE-754-2019
+// maximum (gfx950 v_maximum3_f32), not maxNum
+__device__ __forceinline__ float relu_nan(float x) { return __builtin_elementwise_maximum(x, 0.0f); }
+
 }  // namespace vp

@@ -409,9 +409,13 @@ inline int64_t chunk_of(const vp_handle* h, int64_t B, int64_t T, int64_t H, int
 namespace vpi {
 
 // The bf16 attention kernels compute the capped softmax without a running max: every numerator
-// is exp(l) with |l| <= cap, so the fp32 row sum over S <= 4096 keys stays finite (and exact to
-// rounding) while cap <= 80 (e^80 * 4096 < FLT_MAX).  Other caps take the online-softmax kernel.
-constexpr float kMaxFastCap = 80.0f;
+// is exp(l) with |l| <= cap, and both the row sum and the unnormalised O = sum_s exp(l_s) v_s are
+// accumulated in fp32.  With cap <= 50 (the reference's value for every VideoPrism config,
+// models.py:91) and S <= 4096 keys, |O| <= e^50 * 4096 * max|v| stays below FLT_MAX for any
+// |v| < 1.6e13 -- bf16 activations of a trained model are nowhere near.  (Round 2 allowed 80,
+// priced on the row sum alone: e^80 * S * |v| overflows for |v| > ~1.5 at S = 4096.)  Any other
+// cap (<= 0: no capping, layers.py:586-589; > 50) takes the online-softmax kernel.
+constexpr float kMaxFastCap = 50.0f;
 inline bool fast_cap(float cap) { return cap > 0.0f && cap <= kMaxFastCap; }
 
 // which attention kernel a stack uses (the rest of the pre-LN layer is shared)

@@ -7,26 +7,16 @@ and the reference's fetch path (utils.py:122-142) needs fsspec + egress.
 
 from __future__ import annotations
 
-import collections
 import os
 
 import numpy as np
 
 
 def recover_tree(keys, values):
-    """utils.py:84-105 — nested dict from '/'-separated flat names."""
-    tree = {}
-    sub_trees = collections.defaultdict(list)
-    for k, v in zip(keys, values):
-        if "/" not in k:
-            tree[k] = v
-        else:
-            k_left, k_right = k.split("/", 1)
-            sub_trees[k_left].append((k_right, v))
-    for k, kv_pairs in sub_trees.items():
-        k_subtree, v_subtree = zip(*kv_pairs)
-        tree[k] = recover_tree(k_subtree, v_subtree)
-    return tree
+    """utils.py:84-105 -- nested dict from '/'-separated flat names (the reference's public
+    helper; the tree itself is built by params.unflatten, the package's one implementation)."""
+    from .params import unflatten
+    return unflatten(dict(zip(keys, values)))
 
 
 def npload(fname):
