@@ -125,8 +125,44 @@ def g_full(tag):
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **arrays)
 
 
+# configs[4]'s per-rank workload at full depth: FactorizedVideoCLIP with videoprism_lvt_v1_large
+# (24 + 4 vision layers, 2 auxiliary layers over all 4096 tokens, 12 text layers; encoders.py:762-910,
+# models.py:131-145), B = 1 clip of T = 16 frames, two 64-token texts with the second half of one
+# padded (models_test.py:61-69).  Stored: the video / text embeddings and their similarity
+# (README.md:81) from the fp64 oracle and from its emulation of the reference's bf16 graph, plus
+# the frame embeddings; the GPU tests regenerate weights, video and ids from the stored seeds.
+G8 = dict(cfg="videoprism_lvt_v1_large", vocabulary_size=32000, param_seed=8, video_seed=18, text_seed=28,
+          Q=2, L=64)
+
+
+def g8_text(seed, Q, L, V):
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, V, (Q, L)).astype(np.int32)
+    pads = np.zeros((Q, L), np.float32)
+    pads[1, L // 2:] = 1.0
+    return ids, pads
+
+
+def g8_lvt_large_t16():
+    cfg = dict(models.CONFIGS[G8["cfg"]])
+    cfg["vocabulary_size"] = G8["vocabulary_size"]
+    var = params.synthetic_params(cfg, seed=G8["param_seed"], specs=params.clip_leaf_specs(cfg))
+    x = full_video(G8["video_seed"])
+    ids, pads = g8_text(G8["text_seed"], G8["Q"], G8["L"], cfg["vocabulary_size"])
+    arrays = {k: np.array(v) for k, v in G8.items()}
+    arrays.update(text_token_ids=ids, text_paddings=pads)
+    for mode in ("f64", "bf16"):
+        v, t, out = orc.video_clip(var["params"], cfg, x, ids, pads, mode,
+                                   return_intermediate=("frame_embeddings",))
+        arrays[f"video_emb_{mode}"] = np.asarray(v, np.float64)
+        arrays[f"text_emb_{mode}"] = np.asarray(t, np.float64)
+        arrays[f"similarity_{mode}"] = np.asarray(v, np.float64) @ np.asarray(t, np.float64).T
+        arrays[f"frame_emb_{mode}"] = np.asarray(out["frame_embeddings"], np.float32)
+    np.savez_compressed(os.path.join(HERE, "g8_lvt_large_t16.npz"), **arrays)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7"]
+    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8"]
     if "g1" in which:
         g1_tiny()
     if "g2" in which:
@@ -138,6 +174,8 @@ if __name__ == "__main__":
     for tag in FULL:
         if tag[:2] in which:
             g_full(tag)
+    if "g8" in which:
+        g8_lvt_large_t16()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))
