@@ -111,3 +111,42 @@ def test_rccl_allgather_one_rank(cuda):
         comm.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_bench_base_step_world1_gather_vs_fixture(cuda):
+    """bench.py's real base step at world 1 -- Engine.forward -> op_pool_l2 -> the library's RCCL
+    gather (Communicator.all_gather_rows over a one-rank communicator, bootstrapped through a gloo
+    group as bench.py does) -- on the g6 fixture clip (full Base, T = 16) among 3 others: the
+    gathered row of the fixture clip is within 1e-3 of the fixture's fp64 pooled vector."""
+    import socket
+
+    import torch.distributed as dist
+
+    from videoprism import _native
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "g6_base_t16.npz"),
+                allow_pickle=False)
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    var = params.synthetic_params(cfg, seed=int(g["param_seed"]))
+    eng = models.get_model("videoprism_public_v1_base", fprop_dtype=torch.bfloat16).engine(var, 0)
+    video0 = np.random.default_rng(int(g["video_seed"])).random((1, 16, 288, 288, 3), dtype=np.float32)
+    gen = torch.Generator(device=cuda).manual_seed(1000)
+    video = torch.rand((4, 16, 288, 288, 3), generator=gen, device=cuda).to(torch.bfloat16)
+    video[2] = torch.from_numpy(video0[0]).to(cuda).to(torch.bfloat16)
+    out = torch.empty((4, 4096, 768), dtype=torch.bfloat16, device=cuda)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with distributed.Communicator(0) as comm:
+            eng.forward(video, out=out)
+            rows = comm.all_gather_rows(_native.op_pool_l2(out), counts=[4])
+            torch.cuda.synchronize()
+        assert rows.shape == (4, 768) and rows.dtype == torch.float32
+        err = np.abs(rows[2].double().cpu().numpy() - g["pooled_f64"][0]).max()
+        print(f"bench base step, world 1: gathered pooled row of the fixture clip max-abs {err:.3e}")
+        assert err <= 1e-3
+    finally:
+        dist.destroy_process_group()
