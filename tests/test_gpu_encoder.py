@@ -167,3 +167,27 @@ def test_full_base_b1_bf16_vs_oracle(cuda):
           f"pooled-l2 max-abs {perr.max():.3e}")
     assert perr.max() <= 1e-3
     assert err.mean() <= 3e-2
+
+
+@pytest.mark.parametrize("base", ["videoprism_v1_base", "videoprism_v1_large"])
+def test_temporal_attention_fused_vs_unfused_and_oracle(cuda, base):
+    """bf16 at T = 16 runs the temporal layers' attention inside the q|k|v projection
+    (EPI_QK_TATTN_LN + EPI_V_TATTN_LN); all-zero frame paddings take the unfused path (GEMM ->
+    attn_temporal_kernel) on the same inputs.  Both against the fp64 oracle (2+2 layers, B = 2,
+    clips 2 x 16 x 288 x 288): token mean-abs and pooled max-abs bars as above, and fused vs
+    unfused within bf16 rounding of the probabilities (the fused path rounds the normalised
+    probabilities, the unfused one the numerators)."""
+    cfg = _cfg(base, num_spatial_layers=2, num_temporal_layers=2)
+    var = params.synthetic_params(cfg, seed=31)
+    video = _video(2, 16, 288, 32)
+    fused, _ = _run(cfg, var, video, bf16=True)
+    unfused, _ = _run(cfg, var, video, bf16=True, frame_paddings=np.zeros((2, 16), np.float32))
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    for tag, e in (("fused", fused), ("unfused", unfused)):
+        err = np.abs(e - ref)
+        perr = np.abs(_pool_l2(e) - _pool_l2(ref)).max()
+        print(f"{base} T=16 {tag}: token max-abs {err.max():.3e} mean-abs {err.mean():.3e}; pooled {perr:.3e}")
+        assert err.mean() <= 2e-2 and perr <= 1e-3
+    d = np.abs(fused - unfused)
+    print(f"fused vs unfused: max-abs {d.max():.3e} mean-abs {d.mean():.3e}")
+    assert d.mean() <= 5e-3

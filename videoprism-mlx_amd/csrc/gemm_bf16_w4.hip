@@ -54,6 +54,13 @@ __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
+typedef short w4_s16x4 __attribute__((ext_vector_type(4)));
+// 4 bf16 of one LDS column (rows +0..3 of 16-bit element p) as an MFMA operand
+__device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
+  const w4_s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) w4_s16x4*)(p));
+  return bf16x4{v[0], v[1], v[2], v[3]};
+}
+
 // DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 2 = no ds_reads
 // in the K loop, 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at
 // run time; the accumulators stay live), 16 = after an epilogue the next barrier waits vmcnt(32)
@@ -317,6 +324,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     float4 bl[2], bh[2];
     float4 cl[2], ch[2];  // EPI_*_LN: column sums of W'
     float2 rs[8][2];      // EPI_*_LN: (rstd, -mean*rstd) of rows mt*16 + pass*8 + er
+    float2 rsA[8];        // EPI_*_TATTN_LN: the same for the accumulator rows mt*16 + (lane & 15)
     {
       int ttm, ttn;
       coords(first + j * stride, ttm, ttn);
@@ -326,7 +334,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         bl[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64);
         bh[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64 + 4);
       }
-      if constexpr (EpiTraits<EPI>::kLn) {
+      if constexpr (EpiTraits<EPI>::kQkAttn) {
+        const int mb = ttm * BM + wm * 128 + (lane & 15);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+          rsA[mt] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16));
+      } else if constexpr (EpiTraits<EPI>::kLnVals) {
 #pragma unroll
         for (int nh = 0; nh < 2; ++nh) {
           cl[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64);
@@ -362,6 +375,135 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     using Tr = EpiTraits<EPI>;
     // S3: the A buffer of the tile's last K-tile (free since its h1 barrier; refilled in the next h0)
     char* scr = (S3 ? a_buf(a3 == 0 ? 2 : a3 - 1) : smem + kLds) + w * kScr;
+    if constexpr (Tr::kQkAttn || Tr::kVAttn) {
+      // ---- fused temporal attention (EPI_QK_TATTN_LN / EPI_V_TATTN_LN, see vp_kernels.h).  A
+      // 16-row block mt of this wave's 128 rows is one (b n) sequence of T = 16 frames; the
+      // wave's 128 columns are [q_h | k_h] of one head (QK launch) or v of two heads (V launch).
+      // q, k, v are LN-folded and rounded to bf16 as the reference's bf16 projections are. ----
+      const int r16 = lane & 15, g4 = lane >> 4;
+      if constexpr (Tr::kQkAttn) {
+        // logits^T = K Q^T (16x16x32 on the accumulator-layout operands, d in two halves), capped
+        // softmax over the 16 keys in fp32, the normalised probabilities rounded to bf16 (the
+        // reference's probs.astype(fprop)) and stored as this lane's P^T fragment: keys
+        // 4*g4 .. +3 of query r16, 512 B per (sequence, head).  The LN fold runs on the
+        // accumulators where they stand (lane: row mt*16 + r16, columns 16 nt + 4 g4 + 0..3), so
+        // the operands need no LDS round trip: MFMA k-slot 8*g4 + i <-> column 16*(nt + (i >= 4)) +
+        // 4*g4 + (i & 3), the same map on both operands of a dot product, which leaves it
+        // unchanged.  The logits are summed over two 32-column halves of d (the LN constants of 4
+        // blocks live at a time: 266 us per launch vs 301 with the scratch round trip).
+        float4 cc[4], bb[4];
+        f32x4 x[8];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)  // cc/bb[2*hh + i]: block 2kk + i of q (hh = 0) / k (hh = 1)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const int n = n0 + hh * 64 + 16 * (2 * kk + i) + 4 * g4;
+              cc[2 * hh + i] = *reinterpret_cast<const float4*>(ep.ln_c + n);
+              bb[2 * hh + i] = *reinterpret_cast<const float4*>(ep.bias + n);
+            }
+#pragma unroll
+          for (int mt = 0; mt < 8; ++mt) {
+            auto fold2blk = [&](int hh) {  // operand of blocks (hh*4 + 2kk, +1), constants cc/bb[2hh..]
+              uint32_t u[4];
+#pragma unroll
+              for (int i = 0; i < 2; ++i) {
+                const f32x4& a = acc[hh * 4 + 2 * kk + i][mt];
+                const float4 c = cc[2 * hh + i], b = bb[2 * hh + i];
+                const f32x2_t r = f32x2_t(rsA[mt].x), m = f32x2_t(rsA[mt].y);
+                const f32x2_t lo = __builtin_elementwise_fma(
+                    r, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(m, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
+                const f32x2_t hi = __builtin_elementwise_fma(
+                    r, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(m, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
+                u[2 * i] = pack_bf16x2(lo.x, lo.y);
+                u[2 * i + 1] = pack_bf16x2(hi.x, hi.y);
+              }
+              return *reinterpret_cast<const bf16x8*>(u);
+            };
+            x[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fold2blk(1), fold2blk(0),
+                                                            kk ? x[mt] : f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const float c1 = 2.0f * 1.4426950408889634f / ep.cap, c2 = ep.cap * 1.4426950408889634f;
+        const int head = n0 >> 7;
+        bf16_t* pout = static_cast<bf16_t*>(ep.out);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          // x[mt][r] = logit[query r16][key 4*g4 + r]
+          float p[4], lsum = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[r] = capped_exp_exact(x[mt][r], c1, c2);
+            lsum += p[r];
+          }
+          lsum += __shfl_xor(lsum, 16);
+          lsum += __shfl_xor(lsum, 32);
+          const float inv = 1.0f / lsum;
+          const int64_t sq = (int64_t)(m0 + mt * 16) >> 4;
+          *reinterpret_cast<uint2*>(pout + (sq * ep.heads + head) * 256 + lane * 4) =
+              make_uint2(pack_bf16x2(p[0] * inv, p[1] * inv), pack_bf16x2(p[2] * inv, p[3] * inv));
+        }
+        continue;  // nothing else of this tile is stored
+      } else {
+        // O^T = V^T . P^T per (sequence mt, head nh) on 16x16x16 MFMAs: A = V^T by transposed
+        // reads of the bf16 V block, B = this lane's P^T fragment; the result lands in the
+        // accumulator layout (lane: query r16, d = 16 dt + 4 g4 + r) and replaces v there, so the
+        // store path below writes O with whole-line stores.  The V values take the fp32 scratch
+        // round trip of the store path (row segments, the LN constants of the put layout): folding
+        // them where the accumulators stand measured slower here (register spills, 209 vs 168 us).
+        char* sb0 = scr;
+        char* sb1 = scr + kScrBuf;
+        const bf16_t* pin = static_cast<const bf16_t*>(ep.resid);
+        const int trq = r16 >> 2, trp = r16 & 3;
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          // both heads of sequence mt: V blocks at sb1 and sb1 + 2 KiB, one LDS wait per sequence
+          const int64_t sq = (int64_t)(m0 + mt * 16) >> 4;
+          bf16x4 pb[2];
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+            pb[nh] = *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + nh * 64) >> 6)) * 256 + lane * 4);
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh) {
+            {  // accumulator block -> fp32 scratch (put layout)
+              char* sb = sb0 + frow * 256;
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<f32x4*>(sb + (((q * 4 + (lane >> 4)) ^ (frow & 7)) << 4)) = acc[nh * 4 + q][mt];
+            }
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {  // row segments -> LN fold -> bf16 V rows
+              const int rl = pass * 8 + er;
+              const char* sb = sb0 + rl * 256;
+              const float4 lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
+              const float4 hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
+              const f32x2_t r = f32x2_t(rs[mt][pass].x), m = f32x2_t(rs[mt][pass].y);
+              auto fold2 = [&](float x0, float x1, float c0, float c1, float b0, float b1) {
+                const f32x2_t o = __builtin_elementwise_fma(
+                    r, f32x2_t{x0, x1}, __builtin_elementwise_fma(m, f32x2_t{c0, c1}, f32x2_t{b0, b1}));
+                return pack_bf16x2(o.x, o.y);
+              };
+              *reinterpret_cast<epi_u32x4*>(sb1 + nh * 2048 + rl * 128 + es * 16) =
+                  epi_u32x4{fold2(lo.x, lo.y, cl[nh].x, cl[nh].y, bl[nh].x, bl[nh].y),
+                            fold2(lo.z, lo.w, cl[nh].z, cl[nh].w, bl[nh].z, bl[nh].w),
+                            fold2(hi.x, hi.y, ch[nh].x, ch[nh].y, bh[nh].x, bh[nh].y),
+                            fold2(hi.z, hi.w, ch[nh].z, ch[nh].w, bh[nh].z, bh[nh].w)};
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+              const bf16x4 vf = w4_tr_read(sb1 + nh * 2048 + (4 * g4 + trq) * 128 + (16 * dt + 4 * trp) * 2);
+              acc[nh * 4 + dt][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pb[nh], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            }
+        }
+      }
+    }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)
     F8 ex[2][2][2];  // [buffer][nh][pass]
@@ -426,7 +568,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           fold2(v.lo.z, v.lo.w, cl[nh].z, cl[nh].w, bl[nh].z, bl[nh].w);
           fold2(v.hi.x, v.hi.y, ch[nh].x, ch[nh].y, bh[nh].x, bh[nh].y);
           fold2(v.hi.z, v.hi.w, ch[nh].z, ch[nh].w, bh[nh].z, bh[nh].w);
-        } else {
+        } else if constexpr (!Tr::kVAttn) {  // (fused V launch: the values are O already)
           v.lo.x += bl[nh].x; v.lo.y += bl[nh].y; v.lo.z += bl[nh].z; v.lo.w += bl[nh].w;
           v.hi.x += bh[nh].x; v.hi.y += bh[nh].y; v.hi.z += bh[nh].z; v.hi.w += bh[nh].w;
         }
@@ -557,6 +699,9 @@ hipError_t w4_dispatch_d(int epi, const bf16_t* A, int64_t lda, const bf16_t* W,
       return launch_w4<EPI_RESID_FFN_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST, D>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RELU_BF16: return launch_w4<EPI_RELU_BF16, D>(A, lda, W, ldw, M, N, K, ep, s);
+    // temporal layers' q|k|v projection with the attention fused (T = 16): S3 as the q|k|v GEMM
+    case EPI_QK_TATTN_LN: return launch_w4<EPI_QK_TATTN_LN, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_V_TATTN_LN: return launch_w4<EPI_V_TATTN_LN, D, 0, true>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

@@ -30,6 +30,11 @@ struct EpiTraits {
   static constexpr bool kRelu = EPI == EPI_RELU_BF16;
   static constexpr bool kKeep = kGelu || kRelu || kResidF32 || kResidBf16;
   static constexpr bool kOutBf16 = !(EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN || EPI == EPI_POS_F32);
+  // fused temporal attention (EPI_QK_TATTN_LN / EPI_V_TATTN_LN): LN-fold values per tile as kLn,
+  // custom epilogue in gemm_bf16_w4.hip
+  static constexpr bool kQkAttn = EPI == EPI_QK_TATTN_LN;
+  static constexpr bool kVAttn = EPI == EPI_V_TATTN_LN;
+  static constexpr bool kLnVals = kLn || kQkAttn || kVAttn;
 };
 
 // GELU(x) = x * Phi(x) (exact-erf form, layers.py:31) in one transcendental:

@@ -145,7 +145,7 @@ int vp_finalize(vp_handle* h) {
                        c.num_heads, fold, h->spatial)))
     return rc;
   if ((rc = pack_stack(h, px + "temporal_encoder/transformers_stack/x_layers/", c.num_temporal_layers, D,
-                       c.mlp_dim, c.num_heads, fold, h->temporal)))
+                       c.mlp_dim, c.num_heads, fold, h->temporal, /*qk_perm*/ fold && c.model_dim == c.num_heads * 64)))
     return rc;
   std::vector<float> g(D);
   const char* lns[2] = {"spatial_ln", "temporal_ln"};

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -90,18 +91,25 @@ struct LayerW {  // one transformer layer, packed
   float* c1 = nullptr;
   void* w2 = nullptr;    // [D][F]
   float* b2 = nullptr;
+  // temporal layers (bf16, folded): the q and k rows of wqkv regrouped per head, [q_h | k_h] for
+  // h = 0..heads-1 ([2D][D]), with their b' and c -- the first launch of the fused temporal
+  // attention (EPI_QK_TATTN_LN); the v rows stay at wqkv + 2 D rows
+  void* wqk = nullptr;
+  float* bqk = nullptr;
+  float* cqk = nullptr;
 };
 
 constexpr int kMaxT = 32;
 
 enum ProfClass {
   PC_PATCHIFY = 0, PC_GEMM_PATCH, PC_LAYERNORM, PC_GEMM_QKV, PC_ATTN_SPATIAL, PC_ATTN_TEMPORAL,
-  PC_GEMM_POST, PC_GEMM_FFN1, PC_GEMM_FFN2, PC_ATTN_AUX, PC_ATTN_TEXT, PC_POOL, PC_MISC, PC_COUNT
+  PC_GEMM_POST, PC_GEMM_FFN1, PC_GEMM_FFN2, PC_ATTN_AUX, PC_ATTN_TEXT, PC_POOL, PC_MISC,
+  PC_GEMM_QKV_TATTN, PC_COUNT
 };
 inline const char* kProfNames[PC_COUNT] = {"patchify", "gemm_patch_embed", "layernorm", "gemm_qkv",
                                     "attention_spatial", "attention_temporal", "gemm_post",
                                     "gemm_ffn1_gelu", "gemm_ffn2", "attention_aux", "attention_text",
-                                    "pooler", "misc"};
+                                    "pooler", "misc", "gemm_qkv_temporal_attn"};
 
 // HIP-event profiler: start/stop events around each launch on the launch stream.
 struct Profiler {
@@ -262,7 +270,7 @@ inline std::vector<float> fold_ln(std::vector<float>& w, std::vector<float>& b, 
 // LayerNorms run as kernels (ln*_g / ln*_b).
 template <class H>
 int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH, bool fold,
-               std::vector<LayerW>& out) {
+               std::vector<LayerW>& out, bool qk_perm = false) {
   const float qscale = 1.0f / std::sqrt((float)(D / NH));  // layers.py:576-583
   const auto& lng = param_data(h, pre + "layer_norm/scale");
   const auto& lnb = param_data(h, pre + "layer_norm/bias");
@@ -303,6 +311,21 @@ int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH
     if (fold) {
       const std::vector<float> c = fold_ln(t, tb, g1, be1, 3 * D, D);
       if ((rc = upload_f32(h, c, &lw.cqkv))) return rc;
+      if (qk_perm) {  // [q_h | k_h] per head (rows of the folded t, b', c)
+        const int64_t DH = D / NH;
+        std::vector<float> tq((size_t)2 * D * D), bq((size_t)2 * D), cq((size_t)2 * D);
+        for (int64_t hh = 0; hh < NH; ++hh)
+          for (int which = 0; which < 2; ++which)
+            for (int64_t i = 0; i < DH; ++i) {
+              const int64_t src = which * D + hh * DH + i, dst = hh * 2 * DH + which * DH + i;
+              std::memcpy(tq.data() + (size_t)dst * D, t.data() + (size_t)src * D, (size_t)D * 4);
+              bq[dst] = tb[src];
+              cq[dst] = c[src];
+            }
+        if ((rc = upload_mat(h, tq, &lw.wqk)) || (rc = upload_f32(h, bq, &lw.bqk)) ||
+            (rc = upload_f32(h, cq, &lw.cqk)))
+          return rc;
+      }
     }
     if ((rc = upload_mat(h, t, &lw.wqkv)) || (rc = upload_f32(h, tb, &lw.bqkv))) return rc;
     // post: w[d][n][h] is already [out D][in N*H]
@@ -507,10 +530,31 @@ struct Fwd {
     const bool xbf = bf && !xs_f32;  // residual stream dtype
     const int epi_resid = xbf ? EPI_RESID_BF16 : EPI_RESID_F32;
     const int epi_resid_ffn = xbf ? EPI_RESID_FFN_BF16 : EPI_RESID_FFN;
+    // temporal attention fused into the q|k|v projection (vp_kernels.h EPI_*_TATTN_LN): T = 16
+    // frames (one 16-row MFMA block per sequence), dh = 64, no key paddings, max-free cap
+    // (VP_NO_TATTN=1 in the environment keeps the unfused pair: A/B measurements only)
+    static const bool tattn_off = std::getenv("VP_NO_TATTN") != nullptr;
+    const bool tattn = fold && xbf && kind == ATT_VIDEO && S == 16 && !pad && fast_cap(cap) && D == NH * 64 &&
+                       !layers.empty() && layers[0].wqk && M % 256 == 0 && !tattn_off;
     for (size_t li = 0; li < layers.size(); ++li) {
       LayerW& lw = layers[li];
       const bool last = li + 1 == layers.size();
-      if (fold) {  // LN1 folded: A = the residual stream, (rstd, -mean*rstd) in ln_rs
+      if (tattn) {
+        // P (normalised bf16 probabilities, 512 B per (sequence, head)) goes to `big`; O to hb
+        vp::EpiArgs ep;
+        ep.ln_rs = ln_rs; ep.cap = cap; ep.heads = NH;
+        ep.out = big; ep.bias = lw.bqk; ep.ln_c = lw.cqk;
+        VP_HIP(rec(PC_GEMM_QKV_TATTN, 2.0 * dM * dD * 2 * dD + 4.0 * num_seq * (double)S * S * dD,
+                   gbytes(dD, 2 * dD, 0, 0) + dM * NH * 32.0, [&] {
+          return gemm_bf16_w4(EPI_QK_TATTN_LN, (const bf16_t*)xs, D, (const bf16_t*)lw.wqk, D, M, 2 * D, D, ep, s); }));
+        vp::EpiArgs ev;
+        ev.ln_rs = ln_rs; ev.cap = cap; ev.heads = NH;
+        ev.out = hb; ev.ldo = D; ev.resid = big;
+        ev.bias = lw.bqkv + 2 * D; ev.ln_c = lw.cqkv + 2 * D;
+        const bf16_t* wv = static_cast<const bf16_t*>(lw.wqkv) + (size_t)2 * D * D;
+        VP_HIP(rec(PC_GEMM_QKV_TATTN, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, 0) + dM * NH * 32.0, [&] {
+          return gemm_bf16_w4(EPI_V_TATTN_LN, (const bf16_t*)xs, D, wv, D, M, D, D, ev, s); }));
+      } else if (fold) {  // LN1 folded: A = the residual stream, (rstd, -mean*rstd) in ln_rs
         VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
           return gemm(EPI_BF16_LN, xs, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr,
                       lw.cqkv); }));
@@ -520,7 +564,7 @@ struct Fwd {
         VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
           return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
       }
-      VP_HIP(rec(acls, aflops, abytes, [&] {
+      if (!tattn) VP_HIP(rec(acls, aflops, abytes, [&] {
         if (kind == ATT_TEXT) return attention_masked(big, hb, bf, num_seq, S, NH, cap, pad, causal, s);
         // the bf16 kernels' max-free softmax needs 0 < cap <= kMaxFastCap; cap <= 0 (no capping,
         // layers.py:586-589) or a larger cap runs the online-softmax kernel

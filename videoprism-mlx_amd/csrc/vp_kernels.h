@@ -38,6 +38,19 @@ enum Epilogue {
   // ReLU FFN of the text tower (encoders.py:743): out = relu(acc + bias) * (1 - rowpad);
   // bf16 out on the bf16 GEMM, fp32 out on the fp32 GEMM
   EPI_RELU_BF16 = 13,
+  // temporal self-attention (T = 16 frames, dh = 64, no key paddings) fused into the LN1-folded
+  // q|k|v projection of a temporal layer (layers.py:601-661 over sequences of 16 rows, which are
+  // aligned 16-row blocks of the (b n) t row order): two launches over the same A = x2
+  //  EPI_QK_TATTN_LN: W rows [q_h | k_h] per head (a 256-column tile = 2 heads); the epilogue
+  //    rounds q, k to bf16 (as the reference's bf16 projections), forms the 16x16 logits of every
+  //    (sequence, head) on MFMA, the capped softmax in fp32, and stores the normalised probabilities
+  //    in bf16 -- P^T fragments, 512 B per (sequence, head) at out + ((seq * heads + h) * 256) --
+  //    instead of q and k;
+  //  EPI_V_TATTN_LN: W rows = the v projection; the epilogue rounds v to bf16 and stores
+  //    O = P . V (P from `resid`, the first launch's output) in v's place, so the attention output
+  //    [M][D] comes out of the GEMM and q|k|v never reach HBM.
+  EPI_QK_TATTN_LN = 14,
+  EPI_V_TATTN_LN = 15,
 };
 
 struct EpiArgs {
@@ -53,6 +66,8 @@ struct EpiArgs {
   const float* ln_c = nullptr;    // EPI_*_LN: [N] column sums of W'
   float* st_part = nullptr;       // EPI_*_ST: [N/128][M][2] partial (sum, M2) of each row
   int64_t st_rows = 0;            // EPI_*_ST: M (partial stride)
+  float cap = 0.0f;               // EPI_*_TATTN_LN: logit cap (0 < cap <= 50)
+  int heads = 0;                  // EPI_*_TATTN_LN: heads of the whole projection (P indexing)
 };
 
 // ---- bf16 MFMA GEMM (gemm_bf16.hip) ----
