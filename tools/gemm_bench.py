@@ -168,7 +168,8 @@ def skew(dev, g):
 
 def grouped(dev, g):
     """ffn_layer1 (production LN-folded GELU epilogue) with the N-tile grouped tile order
-    (w4_ngrp) vs the ungrouped one (diag 3011), M = 131072 and the Large shape."""
+    (w4_ngrp) vs the ungrouped one (diag 3011) and the XCD-pair split of W (diag 3013), M = 131072
+    and the Large shape."""
     for name, M, N, K in (("ffn1-base", M_TOK, 3072, 768), ("ffn1-large", 65536, 4096, 1024),
                           ("qkv-large", 65536, 3072, 1024)):
         a, w, b = operands(M, N, K, g, dev)
@@ -179,7 +180,14 @@ def grouped(dev, g):
         fns = {"grouped": lambda: nat.dev_gemm_ln(a, w, b, epi, o, ln_rs=rs, ln_c=c)}
         if epi == nat.EPI_GELU_LN:
             fns["ungrouped"] = lambda: nat.dev_gemm_ln(a, w, b, 3011, o, ln_rs=rs, ln_c=c)
-            fns["gelu-deg6"] = lambda: nat.dev_gemm_ln(a, w, b, 3012, o, ln_rs=rs, ln_c=c)
+            # XCD pairs: each XCD of a pair sweeps the pair's M-blocks over half of W (L2-resident)
+            fns["xcd-pairs"] = lambda: nat.dev_gemm_ln(a, w, b, 3013, o, ln_rs=rs, ln_c=c)
+            o2 = torch.empty_like(o)
+            nat.dev_gemm_ln(a, w, b, epi, o, ln_rs=rs, ln_c=c)
+            nat.dev_gemm_ln(a, w, b, 3013, o2, ln_rs=rs, ln_c=c)
+            torch.cuda.synchronize()
+            print(f"{name}: xcd-pairs == grouped (bitwise):", bool(torch.equal(o, o2)), flush=True)
+            del o2
         res = {k: [] for k in fns}
         for _ in range(3):
             for k, f in fns.items():

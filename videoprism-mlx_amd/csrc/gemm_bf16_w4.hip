@@ -98,6 +98,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // N-tiles, so the group's W rows (<= 2.5 MB) stay in the XCD's 4 MiB L2 instead of the whole W
   // being re-fetched from beyond it for every M-block (ffn_layer1: W = 4.7 MB)
   auto coords = [&](int t, int& tm, int& tn) {
+    if (ngrp < 0) {  // A/B (diag): XCD pairs -- XCD x sweeps the M-blocks of pair x/2 over N-tile half x&1
+      const int per = T >> 3, hn = tilesN >> 1;
+      const int x = t / per, u = t - x * per;
+      const int rm = u / hn;
+      tm = (x >> 1) * ((M / BM) >> 2) + rm;
+      tn = (x & 1) * hn + (u - rm * hn);
+      return;
+    }
     if (ngrp == tilesN) {
       tm = t / tilesN;
       tn = t - tm * tilesN;
@@ -664,7 +672,8 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
-  const int ngrp = (DIAG & 32768) ? N / BN : w4_ngrp(M, N, K, grid);  // DIAG 32768: ungrouped (A/B)
+  // DIAG 32768: ungrouped, 65536: XCD-pair split of W (A/B; needs (M/BM) % 4 == 0, (N/BN) even, grid % 8 == 0)
+  const int ngrp = (DIAG & 32768) ? N / BN : (DIAG & 65536) ? -1 : w4_ngrp(M, N, K, grid);
   VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>));
   hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
                      ldw, M, N, K, ngrp, ep);
@@ -752,6 +761,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 9111: return launch_w4<EPI_RESID_FFN_BF16_ST, 0, kPfLongK>(A, lda, W, ldw, M, N, K, ep, s);
       // the ffn_layer1 production epilogue without the N-tile grouping (A/B of w4_ngrp)
       case 2011: return launch_w4<EPI_GELU_BF16_LN, 512 | 32768>(A, lda, W, ldw, M, N, K, ep, s);
+      // ... and with the XCD-pair order (each XCD of a pair holds half of W in its L2)
+      case 2013: return launch_w4<EPI_GELU_BF16_LN, 512 | 65536>(A, lda, W, ldw, M, N, K, ep, s);
       case 1024: return launch_w4<EPI_BF16, 0, 2>(A, lda, W, ldw, M, N, K, ep, s);
       case 2048: return launch_w4<EPI_BF16, 0, 3>(A, lda, W, ldw, M, N, K, ep, s);
       case 4096: return launch_w4<EPI_BF16, 0, 4>(A, lda, W, ldw, M, N, K, ep, s);

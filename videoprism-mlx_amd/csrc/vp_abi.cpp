@@ -501,8 +501,10 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
                    const float* rowpad, const float* ln_rs, const float* ln_c, float* st_part,
                    void* stream) {
   using namespace vp;
-  if ((epi < EPI_BF16_LN || epi > EPI_POS_BF16_ST) && epi != 3009 && epi != 3010 && epi != 3011 && epi != 10111)
-    return fail(VP_EINVAL, "epilogue must be 8..12 (diag: 3009 ffn1 with the rowpad multiply, 3010 scalar GELU, 3011 ungrouped)");
+  if ((epi < EPI_BF16_LN || epi > EPI_POS_BF16_ST) && epi != 3009 && epi != 3010 && epi != 3011 && epi != 3013 &&
+      epi != 10111)
+    return fail(VP_EINVAL, "epilogue must be 8..12 (diag: 3009 ffn1 with the rowpad multiply, 3010 scalar GELU, "
+                           "3011 ungrouped, 3013 XCD-pair order)");
   const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
