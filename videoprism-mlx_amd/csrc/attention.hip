@@ -58,7 +58,7 @@ constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 // q|k|v layout by strides (elements): row rs, head hs, section (q -> k -> v) sec; the row-major
 // fused projection output is (3D, 64, D), a head-major one (64, M*64, heads*M*64).
 // STAGE: O goes through LDS and leaves as whole 128-B row segments (8 rows per store).
-template <bool MASK, int DIAG = 0, bool STAGE = false, bool PIPE = false>
+template <bool MASK, int DIAG = 0, bool STAGE = false>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
     const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec, CapPoly cp) {
@@ -238,31 +238,16 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   };
 
   chunk_ready(std::integral_constant<int, 0>{});
-  if constexpr (PIPE) {
-    // software pipeline: the S^T MFMAs of tile kt+1 are issued ahead of the numerators of tile kt,
-    // so the matrix pipe works on kt+1 while the transcendental / VALU units work on kt
-    f32x16 xc = qk(0);
+  // (a software-pipelined form -- the S^T MFMAs of tile kt+1 issued ahead of tile kt's
+  // numerators -- is bitwise equal but measured 289.8 vs 206.8 us: at 128 VGPRs it spills inside
+  // the loop)
 #pragma unroll 1
-    for (int cc = 0; cc < 4; ++cc) {
-      const f32x16 xn = qk(2 * cc + 1);
-      pv(2 * cc, xc);
-      if (cc < 3) {
-        if (cc == 0) chunk_ready(std::integral_constant<int, 1>{});
-        else if (cc == 1) chunk_ready(std::integral_constant<int, 2>{});
-        else chunk_ready(std::integral_constant<int, 3>{});
-        xc = qk(2 * cc + 2);
-      }
-      pv(2 * cc + 1, xn);
-    }
-  } else {
-#pragma unroll 1
-    for (int cc = 0; cc < 4; ++cc) {
-      if (cc == 1) chunk_ready(std::integral_constant<int, 1>{});
-      else if (cc == 2) chunk_ready(std::integral_constant<int, 2>{});
-      else if (cc == 3) chunk_ready(std::integral_constant<int, 3>{});
+  for (int cc = 0; cc < 4; ++cc) {
+    if (cc == 1) chunk_ready(std::integral_constant<int, 1>{});
+    else if (cc == 2) chunk_ready(std::integral_constant<int, 2>{});
+    else if (cc == 3) chunk_ready(std::integral_constant<int, 3>{});
 #pragma unroll 2
-      for (int kt = 2 * cc; kt < 2 * cc + 2; ++kt) pv(kt, qk(kt));
-    }
+    for (int kt = 2 * cc; kt < 2 * cc + 2; ++kt) pv(kt, qk(kt));
   }
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;
@@ -523,8 +508,6 @@ hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int nu
     if (diag & 32) return go((const void*)attn_spatial_kernel<false, 0, true>, attn_spatial_kernel<false, 0, true>);
     return go((const void*)attn_spatial_kernel<false, 0, false>, attn_spatial_kernel<false, 0, false>);
   }
-  if (diag == 5000)  // the software-pipelined loop (PIPE) of the production build
-    return go((const void*)attn_spatial_kernel<false, 0, true, true>, attn_spatial_kernel<false, 0, true, true>);
   switch (diag) {
     // memory-pattern ablations on the production (staged-store) build: 8 = Q by whole lines,
     // 64 = no Q loads, 128 = no K/V staging; | 3 = no numerators, no P.V
