@@ -470,7 +470,9 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
     attr[mi] = true;
   }
   const dim3 grid(num_seq * heads);
-  const int rev = 0;  // reverse order measured no faster (the q|k|v stream is HBM-resident either way)
+  // frames in reverse order (the producing GEMM's last-written q|k|v rows first): 2.354-2.358 vs
+  // 2.400-2.407 ms/step in the forward (round 3, one box, alternating; round 2 measured it neutral)
+  const int rev = 1;
   // (a persistent variant -- one workgroup per CU walking (frame, head) pairs, next pair's
   // Q/K/V staged by LDS-DMA during the current one, 160 KiB LDS -- measured 255 vs 218 us: at
   // 2 waves per SIMD the softmax/P.V phase loses more than the continuous stream gains)
