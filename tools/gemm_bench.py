@@ -198,6 +198,22 @@ def grouped(dev, g):
         del a, o
 
 
+def grouped_pmc(dev, g):
+    """The three ffn_layer1 tile orders of `grouped`, 5 launches each and no timing loop, for
+    rocprofv3 --pmc (one kernel symbol per order: FETCH_SIZE per launch is the A/W re-read)."""
+    for name, M, N, K in (("ffn1-base", M_TOK, 3072, 768), ("ffn1-large", 65536, 4096, 1024)):
+        a, w, b = operands(M, N, K, g, dev)
+        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
+        c = torch.zeros(N, device=dev)
+        for code in (nat.EPI_GELU_LN, 3011, 3013):
+            for _ in range(5):
+                nat.dev_gemm_ln(a, w, b, code, o, ln_rs=rs, ln_c=c)
+            torch.cuda.synchronize()
+        print(f"{name}: done", flush=True)
+        del a, o
+
+
 def s3_ab(dev, g):
     """ffn_layer2 shape: S3 staging (production for K >= 2048: three A buffers, A pieces in h0)
     vs the PF 2 build it replaced -- plain epilogue, no epilogue, and the production residual +
@@ -232,6 +248,8 @@ def main():
         variants(dev, g, 4, [0, 8, 32, 5000, 5001, 5002, 5003])
     elif mode == "grouped":
         grouped(dev, g)
+    elif mode == "grouped_pmc":
+        grouped_pmc(dev, g)
     elif mode == "s3":
         s3_ab(dev, g)
     elif mode == "skew":
