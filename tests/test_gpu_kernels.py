@@ -438,48 +438,3 @@ def test_gemm_row_stats(cuda, epi):
     assert torch.allclose(rs_p.double(), ref, rtol=2e-5, atol=1e-5)
     assert torch.allclose(rs_r.double(), ref, rtol=2e-5, atol=1e-5)
 
-
-
-# W-direct GEMM (gemm_bf16_w4.hip WD: W fragments from a pre-packed copy straight into registers,
-# only A staged through LDS): the same MFMA sequence on the same operands, so every forward
-# epilogue must equal the LDS-staged kernel's output bit for bit.  Shapes: the forward's (persistent,
-# N-tile grouped at (4096, 3072, 768)), K = 3072, and odd tile / K-tile counts (1280, 768, 704).
-WD_SHAPES = [(4096, 3072, 768), (2048, 768, 3072), (1280, 768, 704), (512, 2304, 768)]
-
-
-@pytest.mark.parametrize("M,N,K", WD_SHAPES)
-@pytest.mark.parametrize("epi,rowpad", [(nat.EPI_BF16_LN, False), (nat.EPI_GELU_LN, False), (nat.EPI_GELU_LN, True),
-                                        (nat.EPI_RESID_BF16_ST, True), (nat.EPI_RESID_FFN_BF16_ST, True),
-                                        (nat.EPI_RESID_FFN_BF16, True), (nat.EPI_STORE, False)])
-def test_gemm_wdirect_bitwise(cuda, M, N, K, epi, rowpad):
-    g = torch.Generator(device="cpu").manual_seed(M + 3 * N + K + epi)
-    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
-    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
-    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
-    pad = (torch.rand(M, generator=g) < 0.2).float().to(cuda) if rowpad else None
-    rs = torch.stack([torch.rand(M, generator=g) + 0.5, torch.randn(M, generator=g) * 0.3], 1).contiguous().to(cuda)
-    c = torch.randn(N, generator=g).to(cuda)
-    x0 = _bf(torch.randn(M, N, generator=g)).to(cuda)
-    resid = epi in (nat.EPI_RESID_BF16_ST, nat.EPI_RESID_FFN_BF16_ST, nat.EPI_RESID_FFN_BF16)
-    st = epi in (nat.EPI_RESID_BF16_ST, nat.EPI_RESID_FFN_BF16_ST)
-    wf = nat.pack_frag(w)
-    outs, parts = [], []
-    for wd in (False, True):
-        o = x0.clone() if resid else torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-        part = torch.zeros(N // 128, M, 2, device=cuda) if st else None
-        if wd:
-            nat.dev_gemm_wd(a, wf, b, epi, o, resid=o if resid else None, rowpad=pad, ln_rs=rs, ln_c=c, st_part=part)
-        elif epi in (nat.EPI_STORE, nat.EPI_RESID_FFN_BF16):
-            nat.dev_gemm_kernel(4, a, w, b, epi, o, resid=o if resid else None, rowpad=pad)
-        else:
-            nat.dev_gemm_ln(a, w, b, epi, o, resid=o if resid else None, rowpad=pad, ln_rs=rs, ln_c=c, st_part=part)
-        outs.append(o)
-        parts.append(part)
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
-    if st:
-        assert torch.equal(parts[0], parts[1])
-    if epi == nat.EPI_STORE:  # and against fp64 once
-        ref = a.double() @ w.double().T + b.double()
-        err = (outs[1].double() - ref).abs()
-        assert torch.all(err <= 2 ** -8 * ref.abs() + 1e-3), float(err.max())

@@ -86,8 +86,9 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // 7.78 -> 7.48 ms/step in the forward (tools/gemm_bench.py s3).  (Three A stages with all 16
 // pieces in h1 measured 468 vs 475 us isolated and nothing in the forward; the lead time alone is
 // not it -- spreading the pieces over both phases is.)
-// WD (W direct): W comes pre-packed in MFMA-fragment order (`w4_pack_frag`: per 128-column group
-// and 32-deep k-chunk, 8 fragments x 64 lanes x 16 B = 8 KiB contiguous) and each wave loads its
+// WD (W direct; diag builds only, measured 10-15 % slower than LDS-staged W):
+// W comes pre-packed in MFMA-fragment order (per 128-column group and 32-deep k-chunk, 8 fragments
+// x 64 lanes x 16 B = 8 KiB contiguous; tools/gemm_bench.py pack_frag) and each wave loads its
 // W fragments with buffer_load_dwordx4 straight into VGPRs -- one full-line 1 KiB request per
 // fragment, no LDS-DMA piece and no ds_read for W.  Only A goes through LDS (8 pieces and 8
 // ds_reads per K-tile and wave instead of 16 + 16).  W fragments of k-half (g, h1) are requested
@@ -853,49 +854,12 @@ hipError_t w4_dispatch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, i
 }
 }  // namespace
 
-namespace {
-// W-direct builds (ep.wfrag: W in w4_pack_frag order), 2-stage A staging
-hipError_t w4_dispatch_wd(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
-                          int K, const EpiArgs& ep, hipStream_t s) {
-  switch (epi) {
-    case EPI_BF16: return launch_w4<EPI_BF16, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_BF16_LN: return launch_w4<EPI_BF16_LN, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_GELU_BF16_LN:
-      if (!ep.rowpad) return launch_w4<EPI_GELU_BF16_LN, 512, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-      return launch_w4<EPI_GELU_BF16_LN, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_BF16_ST: return launch_w4<EPI_RESID_BF16_ST, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN_BF16: return launch_w4<EPI_RESID_FFN_BF16, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN_BF16_ST:
-      return launch_w4<EPI_RESID_FFN_BF16_ST, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_QK_TATTN_LN: return launch_w4<EPI_QK_TATTN_LN, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_V_TATTN_LN: return launch_w4<EPI_V_TATTN_LN, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-  }
-  return hipErrorInvalidValue;
-}
-}  // namespace
-
-void w4_pack_frag(const uint16_t* W, int64_t N, int64_t K, uint16_t* out) {
-  const int64_t nkc = K / 32;
-  for (int64_t ng = 0; ng < N / 128; ++ng)
-    for (int64_t kc = 0; kc < nkc; ++kc)
-      for (int64_t nt = 0; nt < 8; ++nt)
-        for (int64_t lane = 0; lane < 64; ++lane) {
-          const int64_t n = ng * 128 + nt * 16 + (lane & 15), k = kc * 32 + (lane >> 4) * 8;
-          uint16_t* d = out + (((ng * nkc + kc) * 8 + nt) * 64 + lane) * 8;
-          for (int e = 0; e < 8; ++e) d[e] = W[n * K + k + e];
-        }
-}
-
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s) {
   // byte offsets into A / W must fit the 32-bit buffer range
   if ((uint64_t)M * (uint64_t)lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * (uint64_t)ldw * 2 >= 0xFFFFFFF0ull)
     return hipErrorInvalidValue;
   if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
-  if (ep.wfrag) {
-    if (ldw != K) return hipErrorInvalidValue;  // the packed W has no row stride
-    return w4_dispatch_wd(epi, A, lda, W, ldw, M, N, K, ep, s);
-  }
 #ifdef VP_DIAG
   if (epi >= 1000) {  // ablation builds (tools' diag library only), EPI_BF16 epilogue
     switch (epi - 1000) {
@@ -933,7 +897,8 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 2009: return launch_w4<EPI_GELU_BF16_LN, 0>(A, lda, W, ldw, M, N, K, ep, s);
       // + scalar (unpacked) GELU arithmetic
       case 2010: return launch_w4<EPI_GELU_BF16_LN, 512 | 1024>(A, lda, W, ldw, M, N, K, ep, s);
-      // W-direct builds (W pre-packed by w4_pack_frag): plain / no epilogue / no A staging
+      // W-direct builds (W pre-packed in fragment order, tools/gemm_bench.py pack_frag): plain / no
+      // epilogue / no A staging -- measured slower than the LDS-staged W
       case 7000: return launch_w4<EPI_BF16, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
       case 7008: return launch_w4<EPI_BF16, 8, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
       case 7004: return launch_w4<EPI_BF16, 4, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);

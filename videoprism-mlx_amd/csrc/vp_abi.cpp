@@ -516,31 +516,6 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
   return VP_OK;
 }
 
-// Not in the public header: the W-direct GEMM (gemm_bf16_w4.hip WD) with a forward epilogue over a
-// W already in fragment order (tests/test_gpu_kernels.py: bitwise against vp_dev_gemm_ln), and the
-// host packer that produces that order (vp_finalize uses the same function).
-int vp_dev_gemm_wd(int epi, const void* A, const void* Wfrag, int64_t M, int64_t N, int64_t K, void* out,
-                   const float* bias, const void* resid, const float* rowpad, const float* ln_rs,
-                   const float* ln_c, float* st_part, float cap, int heads, void* stream) {
-  using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
-  if (M % 256 || N % 256) return fail(VP_EINVAL, "W-direct GEMM: M and N must be multiples of 256");
-  EpiArgs ep;
-  ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N; ep.rowpad = rowpad;
-  ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.st_part = st_part; ep.st_rows = M;
-  ep.cap = cap; ep.heads = heads; ep.wfrag = 1;
-  VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)Wfrag, K, (int)M, (int)N, (int)K, ep,
-                      static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-
-int vp_dev_pack_frag(const uint16_t* W, int64_t N, int64_t K, uint16_t* out) {
-  if (!W || !out || N <= 0 || K <= 0 || N % 128 || K % 32) return fail(VP_EINVAL, "pack_frag: N % 128, K % 32");
-  vp::w4_pack_frag(W, N, K, out);
-  return VP_OK;
-}
-
 #ifdef VP_DIAG
 // diag library only: the fused q|k|v projection + spatial attention kernel (an experiment that
 // measured no faster than the unfused pair; tools/qa_bench.py checks it bitwise

@@ -97,9 +97,6 @@ struct LayerW {  // one transformer layer, packed
   void* wqk = nullptr;
   float* bqk = nullptr;
   float* cqk = nullptr;
-  // the same bf16 matrices in the W-direct fragment order of gemm_bf16_w4 (w4_pack_frag; bf16
-  // folded stacks): what the forward's GEMMs read unless VP_W4_LDS_W=1 (A/B only)
-  void *wqkv_f = nullptr, *wpost_f = nullptr, *w1_f = nullptr, *w2_f = nullptr, *wqk_f = nullptr;
 };
 
 constexpr int kMaxT = 32;
@@ -189,21 +186,6 @@ int upload_mat(H* h, const std::vector<float>& v, void** out) {
   int rc = dev_alloc(h, b.size() * 2, &p);
   if (rc) return rc;
   VP_HIP(hipMemcpy(p, b.data(), b.size() * 2, hipMemcpyHostToDevice));
-  *out = p;
-  return VP_OK;
-}
-
-// bf16 matrix [N][K] in the W-direct fragment order (w4_pack_frag); needs N % 128 == 0, K % 32 == 0
-template <class H>
-int upload_frag(H* h, const std::vector<float>& v, int64_t N, int64_t K, void** out) {
-  if (N % 128 || K % 32) return fail(VP_EINVAL, "upload_frag: N % 128 / K % 32");
-  std::vector<uint16_t> b(v.size()), f(v.size());
-  for (size_t i = 0; i < v.size(); ++i) b[i] = host_f2bf(v[i]);
-  vp::w4_pack_frag(b.data(), N, K, f.data());
-  void* p;
-  int rc = dev_alloc(h, f.size() * 2, &p);
-  if (rc) return rc;
-  VP_HIP(hipMemcpy(p, f.data(), f.size() * 2, hipMemcpyHostToDevice));
   *out = p;
   return VP_OK;
 }
@@ -341,20 +323,15 @@ int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH
               cq[dst] = c[src];
             }
         if ((rc = upload_mat(h, tq, &lw.wqk)) || (rc = upload_f32(h, bq, &lw.bqk)) ||
-            (rc = upload_f32(h, cq, &lw.cqk)) ||
-            (D % 128 == 0 && (rc = upload_frag(h, tq, 2 * D, D, &lw.wqk_f))))
+            (rc = upload_f32(h, cq, &lw.cqk)))
           return rc;
       }
     }
     if ((rc = upload_mat(h, t, &lw.wqkv)) || (rc = upload_f32(h, tb, &lw.bqkv))) return rc;
-    // W-direct copies: the folded bf16 stacks (vision and auxiliary encoders) when the shapes allow
-    const bool frag = fold && h->bf16() && D % 128 == 0 && F % 128 == 0;
-    if (frag && (rc = upload_frag(h, t, 3 * D, D, &lw.wqkv_f))) return rc;
     // post: w[d][n][h] is already [out D][in N*H]
     std::vector<float> wp(wpost.begin() + (size_t)l * D * D, wpost.begin() + (size_t)(l + 1) * D * D);
     std::vector<float> bp(bpost.begin() + (size_t)l * D, bpost.begin() + (size_t)(l + 1) * D);
     if ((rc = upload_mat(h, wp, &lw.wpost)) || (rc = upload_f32(h, bp, &lw.bpost))) return rc;
-    if (frag && (rc = upload_frag(h, wp, D, D, &lw.wpost_f))) return rc;
     if ((rc = upload_f32(h, g1, &lw.ln1_g)) || (rc = upload_f32(h, be1, &lw.ln1_b)) ||
         (rc = upload_f32(h, g2, &lw.ln2_g)) || (rc = upload_f32(h, be2, &lw.ln2_b)))
       return rc;
@@ -374,7 +351,6 @@ int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH
     if ((rc = upload_mat(h, t1, &lw.w1)) || (rc = upload_f32(h, bb1, &lw.b1)) ||
         (rc = upload_mat(h, t2, &lw.w2)) || (rc = upload_f32(h, bb2, &lw.b2)))
       return rc;
-    if (frag && ((rc = upload_frag(h, t1, F, D, &lw.w1_f)) || (rc = upload_frag(h, t2, D, F, &lw.w2_f)))) return rc;
   }
   return VP_OK;
 }
@@ -523,15 +499,11 @@ struct Fwd {
 
   hipError_t gemm(int epi, const void* A, int K, const void* Wt, int N, void* o, int64_t ldo, const float* bias,
                   const void* resid, const float* pos, int pos_rows, const float* rowpad,
-                  const float* lnc = nullptr, const void* Wfrag = nullptr) const {
+                  const float* lnc = nullptr) const {
     vp::EpiArgs ep;
     ep.out = o; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldo;
     ep.pos = pos; ep.pos_rows = pos_rows; ep.rowpad = rowpad;
     ep.ln_rs = ln_rs; ep.ln_c = lnc; ep.st_part = st_part; ep.st_rows = M;
-    if (bf && Wfrag && M % 256 == 0 && N % 256 == 0) {  // W-direct 4-wave kernel (gemm_bf16_w4.hip WD)
-      ep.wfrag = 1;
-      return vp::gemm_bf16_w4(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wfrag, K, M, N, K, ep, s);
-    }
     if (bf) return vp::gemm_bf16_auto(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wt, K, M, N, K, ep, s);
     return vp::gemm_f32(epi, (const float*)A, K, (const float*)Wt, K, M, N, K, ep, s);
   }
@@ -562,10 +534,6 @@ struct Fwd {
     // frames (one 16-row MFMA block per sequence), dh = 64, no key paddings, max-free cap
     // (VP_NO_TATTN=1 in the environment keeps the unfused pair: A/B measurements only)
     static const bool tattn_off = std::getenv("VP_NO_TATTN") != nullptr;
-    // W-direct GEMMs (W fragments straight from L2 into registers, gemm_bf16_w4.hip WD) wherever
-    // the stack holds the fragment-order copies, when VP_W4_WD=1 (under measurement)
-    static const bool wd_off = std::getenv("VP_W4_WD") == nullptr;
-    auto wf = [&](const void* p) { return wd_off ? nullptr : p; };
     const bool tattn = fold && xbf && kind == ATT_VIDEO && S == 16 && !pad && fast_cap(cap) && D == NH * 64 &&
                        !layers.empty() && layers[0].wqk && M % 256 == 0 && !tattn_off;
     for (size_t li = 0; li < layers.size(); ++li) {
@@ -578,25 +546,18 @@ struct Fwd {
         ep.out = big; ep.bias = lw.bqk; ep.ln_c = lw.cqk;
         VP_HIP(rec(PC_GEMM_QKV_TATTN, 2.0 * dM * dD * 2 * dD + 4.0 * num_seq * (double)S * S * dD,
                    gbytes(dD, 2 * dD, 0, 0) + dM * NH * 32.0, [&] {
-          if (wf(lw.wqk_f)) {
-            ep.wfrag = 1;
-            return gemm_bf16_w4(EPI_QK_TATTN_LN, (const bf16_t*)xs, D, (const bf16_t*)lw.wqk_f, D, M, 2 * D, D, ep, s);
-          }
           return gemm_bf16_w4(EPI_QK_TATTN_LN, (const bf16_t*)xs, D, (const bf16_t*)lw.wqk, D, M, 2 * D, D, ep, s); }));
         vp::EpiArgs ev;
         ev.ln_rs = ln_rs; ev.cap = cap; ev.heads = NH;
         ev.out = hb; ev.ldo = D; ev.resid = big;
         ev.bias = lw.bqkv + 2 * D; ev.ln_c = lw.cqkv + 2 * D;
-        // (the v rows start 2D rows in; the fragment order keeps whole 128-row groups contiguous,
-        // so the offset is the same in both layouts)
-        if (wf(lw.wqkv_f)) ev.wfrag = 1;
-        const bf16_t* wv = static_cast<const bf16_t*>(ev.wfrag ? lw.wqkv_f : lw.wqkv) + (size_t)2 * D * D;
+        const bf16_t* wv = static_cast<const bf16_t*>(lw.wqkv) + (size_t)2 * D * D;
         VP_HIP(rec(PC_GEMM_QKV_TATTN, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, 0) + dM * NH * 32.0, [&] {
           return gemm_bf16_w4(EPI_V_TATTN_LN, (const bf16_t*)xs, D, wv, D, M, D, D, ev, s); }));
       } else if (fold) {  // LN1 folded: A = the residual stream, (rstd, -mean*rstd) in ln_rs
         VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
           return gemm(EPI_BF16_LN, xs, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr,
-                      lw.cqkv, wf(lw.wqkv_f)); }));
+                      lw.cqkv); }));
       } else {
         VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
           return layernorm(xs, xbf, M, D, lw.ln1_g, lw.ln1_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
@@ -622,12 +583,11 @@ struct Fwd {
         return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s); }));
       VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {
         return gemm(fold ? EPI_RESID_BF16_ST : epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1,
-                    nullptr, nullptr, fold ? wf(lw.wpost_f) : nullptr); }));
+                    nullptr); }));
       if (fold) {  // LN2 folded into ffn_layer1
         VP_HIP(finalize());
         VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
-          return gemm(EPI_GELU_BF16_LN, xs, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad, lw.c1,
-                      wf(lw.w1_f)); }));
+          return gemm(EPI_GELU_BF16_LN, xs, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad, lw.c1); }));
       } else {
         VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
           return layernorm(xs, xbf, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
@@ -638,7 +598,7 @@ struct Fwd {
       const bool st = fold && !last;  // the next layer's LN1 statistics
       VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, dE, dE), [&] {
         return gemm(st ? EPI_RESID_FFN_BF16_ST : epi_resid_ffn, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1,
-                    pad, nullptr, fold && xbf ? wf(lw.w2_f) : nullptr); }));
+                    pad); }));
       if (st) VP_HIP(finalize());
     }
     return VP_OK;

@@ -68,7 +68,6 @@ struct EpiArgs {
   int64_t st_rows = 0;            // EPI_*_ST: M (partial stride)
   float cap = 0.0f;               // EPI_*_TATTN_LN: logit cap (0 < cap <= 50)
   int heads = 0;                  // EPI_*_TATTN_LN: heads of the whole projection (P indexing)
-  int wfrag = 0;                  // gemm_bf16_w4 only: W is in the W-direct fragment order (w4_pack_frag)
 };
 
 // ---- bf16 MFMA GEMM (gemm_bf16.hip) ----
@@ -80,10 +79,6 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 // staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
-// W [N][K] row-major bf16 -> the W-direct order gemm_bf16_w4 reads when ep.wfrag is set: per
-// 128-row group and 32-deep k-chunk, 8 MFMA fragments (16 rows each) of 64 lanes x 8 bf16, lane
-// = (k-octet in the chunk) * 16 + row in the fragment (N % 128 == 0, K % 32 == 0; host side)
-void w4_pack_frag(const uint16_t* W, int64_t N, int64_t K, uint16_t* out);
 // [diag library only] 4-wave, 256x128 tile, two accumulator sets: the epilogue of tile j runs under the MFMAs of
 // tile j+1 (gemm_bf16_ov.hip).  bf16-output epilogues, M % 256, N % 128, K % 64, K >= 704.
 bool gemm_bf16_ov_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw);

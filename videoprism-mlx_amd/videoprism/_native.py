@@ -139,9 +139,6 @@ _SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
-    "vp_dev_gemm_wd": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
-                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p]),
-    "vp_dev_pack_frag": (c_int, [c_void_p, c_int64, c_int64, c_void_p]),
 }
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
@@ -274,28 +271,6 @@ def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln
          _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad), _ptr(ln_rs), _ptr(ln_c),
          _ptr(st_part), _stream(stream))
     return out
-
-
-def dev_gemm_wd(a, wfrag, bias, epilogue, out, resid=None, rowpad=None, ln_rs=None, ln_c=None,
-                st_part=None, cap=0.0, heads=0, stream=None):
-    """The W-direct bf16 GEMM (gemm_bf16_w4.hip WD) with a forward epilogue; `wfrag` is W [N,K] in
-    fragment order (`pack_frag`), all tensors contiguous on the device."""
-    M, K = a.shape
-    N = wfrag.shape[0]
-    call("vp_dev_gemm_wd", epilogue, _ptr(a), _ptr(wfrag), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
-         _ptr(rowpad), _ptr(ln_rs), _ptr(ln_c), _ptr(st_part), float(cap), int(heads), _stream(stream))
-    return out
-
-
-def pack_frag(w):
-    """W [N,K] bf16 (torch, any device) -> the W-direct fragment order, same shape, through the
-    library's host packer (the one vp_finalize uses)."""
-    import torch
-    N, K = w.shape
-    src = w.detach().to("cpu", torch.bfloat16).contiguous()
-    dst = torch.empty_like(src)
-    call("vp_dev_pack_frag", src.data_ptr(), N, K, dst.data_ptr())
-    return dst.to(w.device)
 
 
 def dev_qkv_attention(x, ln_rs, wqkv, bias, lnc, out, frames, heads, cap, stream=None):
