@@ -310,6 +310,9 @@ def main():
         variants(dev, g, 4, [0, 128, 4, 8, 136, 12])
     elif mode == "w8var":
         variants(dev, g, 8, [0, 1, 2, 8, 16])
+    elif mode == "w8epi":  # 8-wave kernel with / without its epilogue (32), and without staging (33) / reads (34)
+        variants(dev, g, 8, [0, 32, 33, 34])
+        variants(dev, g, 4, [0, 8, 12])
     else:
         compare(dev, g)
 

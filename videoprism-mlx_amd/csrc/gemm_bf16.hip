@@ -60,7 +60,7 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 1 = no glds in
 // the K loop, 2 = no ds_reads in the K loop, 4 = no barriers in the K loop, 8 = glds issued
 // but no vmcnt wait in the K loop, 16 = register staging (global_load_dwordx4 two phases
-// ahead, ds_write_b128 when the region is free) instead of global_load_lds.
+// ahead, ds_write_b128 when the region is free) instead of global_load_lds, 32 = no epilogue.
 template <int EPI, int DIAG = 0>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -293,6 +293,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     // ---- epilogue of tile j: lane holds D[n = nb + 16*ng + 4*(lane>>4) + r][m = mb + 16*mg] ----
     const int tile = first + j * stride;
     ++j;
+    if constexpr (DIAG & 32) {  // ablation: no epilogue (the accumulators stay live)
+      if (ep.ldo != -12345) continue;
+    }
     const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
     const int mb = m0 + wm * 128 + l16;
     const int nbase = n0 + wn * 64 + cq * 4;
@@ -381,6 +384,9 @@ hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* 
     case 8: return launch_one<EPI_BF16, 8>(A, lda, W, ldw, M, N, K, ep, s);
     case 10: return launch_one<EPI_BF16, 10>(A, lda, W, ldw, M, N, K, ep, s);
     case 16: return launch_one<EPI_BF16, 16>(A, lda, W, ldw, M, N, K, ep, s);
+    case 32: return launch_one<EPI_BF16, 32>(A, lda, W, ldw, M, N, K, ep, s);
+    case 33: return launch_one<EPI_BF16, 33>(A, lda, W, ldw, M, N, K, ep, s);
+    case 34: return launch_one<EPI_BF16, 34>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }
