@@ -277,6 +277,35 @@ def wd_ab(dev, g):
         del a, w, wp, o1, o2
 
 
+def w8b_ab(dev, g):
+    """8-wave kernel with the 4-wave pipeline (gemm_bf16_w8b.hip) vs the 4-wave kernel: ffn_layer1's
+    production epilogue (LN fold + GELU), the plain epilogue and no epilogue, at the forward's shapes."""
+    for name, M, N, K in (("ffn1", M_TOK, 3072, 768), ("qkv", M_TOK, 2304, 768), ("ffn1-large", 65536, 4096, 1024)):
+        a, w, b = operands(M, N, K, g, dev)
+        o1 = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+        o2 = torch.empty_like(o1)
+        rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
+        c = torch.zeros(N, device=dev)
+        nat.dev_gemm_ln(a, w, b, nat.EPI_GELU_LN, o1, ln_rs=rs, ln_c=c)
+        nat.dev_gemm_w8b(a, w, b, nat.EPI_GELU_LN, o2, ln_rs=rs, ln_c=c)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(o1, o2))
+        fns = {"w4-gelu-ln": lambda: nat.dev_gemm_ln(a, w, b, nat.EPI_GELU_LN, o1, ln_rs=rs, ln_c=c),
+               "w8b-gelu-ln": lambda: nat.dev_gemm_w8b(a, w, b, nat.EPI_GELU_LN, o2, ln_rs=rs, ln_c=c),
+               "w4-bf16": lambda: nat.dev_gemm_kernel(4, a, w, b, 0, o1),
+               "w8b-bf16": lambda: nat.dev_gemm_w8b(a, w, b, 0, o2),
+               "w4-noepi": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 8, o1),
+               "w8b-noepi": lambda: nat.dev_gemm_w8b(a, w, b, 0, o2, diag=8)}
+        res = {k: [] for k in fns}
+        for _ in range(3):
+            for k, f in fns.items():
+                res[k].append(timeit(f, iters=10, warm=2))
+        flop = 2.0 * M * N * K
+        print(f"{name} w8b==w4 (gelu-ln): {same}: " + " | ".join(
+            f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
+        del a, w, o1, o2
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -293,6 +322,8 @@ def main():
         s3_ab(dev, g)
     elif mode == "wd":
         wd_ab(dev, g)
+    elif mode == "w8b":
+        w8b_ab(dev, g)
     elif mode == "skew":
         skew(dev, g)
     elif mode == "msize":

@@ -771,22 +771,6 @@ int num_cus_w4() {
   return n;
 }
 
-// N-tile group size (see coords): the whole W when it is small (<= 2 MB) or when the GEMM streams
-// A from HBM (K >= 2048: a group sweep would re-read A per group); else groups whose W rows take
-// <= 2.5 MB (W > 4 MB: Base ffn_layer1 6 of 12 N-tiles, Large ffn_layer1 / q|k|v 4) or <= half of
-// W (Base q|k|v, 3.5 MB: 3 of 9; forward 6.39 -> 6.29 ms/step, one box, alternating runs)
-int w4_ngrp(int M, int N, int K, int grid) {
-  const int tilesN = N / BN;
-  const int64_t w_tile = (int64_t)BN * K * 2;  // W bytes per N-tile
-  const int64_t w_all = (int64_t)tilesN * w_tile;
-  if (w_all <= (2ll << 20) || K >= 2048 || (M / BM) % 8 || grid % 8) return tilesN;
-  const int64_t budget = w_all > (4ll << 20) ? (5ll << 19) : w_all / 2;
-  int g = tilesN;
-  for (int d = tilesN; d >= 1; --d)
-    if (tilesN % d == 0 && (int64_t)d * w_tile <= budget) { g = d; break; }
-  return g;
-}
-
 template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false, bool WD = false>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
@@ -808,6 +792,22 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
 }
 
 }  // namespace
+
+// N-tile group size (see coords): the whole W when it is small (<= 2 MB) or when the GEMM streams
+// A from HBM (K >= 2048: a group sweep would re-read A per group); else groups whose W rows take
+// <= 2.5 MB (W > 4 MB: Base ffn_layer1 6 of 12 N-tiles, Large ffn_layer1 / q|k|v 4) or <= half of
+// W (Base q|k|v, 3.5 MB: 3 of 9; forward 6.39 -> 6.29 ms/step, one box, alternating runs)
+int w4_ngrp(int M, int N, int K, int grid) {
+  const int tilesN = N / BN;
+  const int64_t w_tile = (int64_t)BN * K * 2;  // W bytes per N-tile
+  const int64_t w_all = (int64_t)tilesN * w_tile;
+  if (w_all <= (2ll << 20) || K >= 2048 || (M / BM) % 8 || grid % 8) return tilesN;
+  const int64_t budget = w_all > (4ll << 20) ? (5ll << 19) : w_all / 2;
+  int g = tilesN;
+  for (int d = tilesN; d >= 1; --d)
+    if (tilesN % d == 0 && (int64_t)d * w_tile <= budget) { g = d; break; }
+  return g;
+}
 
 namespace {
 // production epilogues; D = 0: nontemporal output stores, D = 256: plain stores (ablation)

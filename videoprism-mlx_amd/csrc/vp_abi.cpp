@@ -517,6 +517,20 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
 }
 
 #ifdef VP_DIAG
+// diag library only: the 8-wave GEMM with the 4-wave pipeline (tools/diag/csrc/gemm_bf16_w8b.hip),
+// EPI_BF16 / EPI_GELU_BF16_LN, for tools/ab_tests.py and tools/gemm_bench.py w8b (diag 8: no epilogue)
+int vp_dev_gemm_w8b(int epi, int diag, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
+                    const float* bias, const float* rowpad, const float* ln_rs, const float* ln_c, void* stream) {
+  using namespace vp;
+  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  if (e) return fail(VP_EINVAL, e);
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias; ep.rowpad = rowpad; ep.ln_rs = ln_rs; ep.ln_c = ln_c;
+  VP_HIP(gemm_bf16_w8b(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, diag,
+                       static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // diag library only: the fused q|k|v projection + spatial attention kernel (an experiment that
 // measured no faster than the unfused pair; tools/qa_bench.py checks it bitwise
 // against vp_dev_gemm_ln(EPI_BF16_LN) + vp_op_attention)

@@ -79,6 +79,12 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 // staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
+// N-tile group size of the persistent tile order (gemm_bf16_w4.hip; shared by gemm_bf16_w8b)
+int w4_ngrp(int M, int N, int K, int grid);
+// diag library only: 8-wave form of the 4-wave kernel's pipeline (two 128x64 waves per SIMD,
+// tools/diag/csrc/gemm_bf16_w8b.hip): EPI_BF16 / EPI_GELU_BF16_LN; diag 8 = no epilogue
+hipError_t gemm_bf16_w8b(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
+                         int K, const EpiArgs& ep, int diag, hipStream_t s);
 // [diag library only] 4-wave, 256x128 tile, two accumulator sets: the epilogue of tile j runs under the MFMAs of
 // tile j+1 (gemm_bf16_ov.hip).  bf16-output epilogues, M % 256, N % 128, K % 64, K >= 704.
 bool gemm_bf16_ov_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw);

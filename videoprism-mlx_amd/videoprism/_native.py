@@ -142,6 +142,8 @@ _SIGNATURES = {
 }
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
+    "vp_dev_gemm_w8b": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p]),
     "vp_dev_attention_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_attention_qh": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
@@ -270,6 +272,16 @@ def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln
     call("vp_dev_gemm_ln", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
          _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad), _ptr(ln_rs), _ptr(ln_c),
          _ptr(st_part), _stream(stream))
+    return out
+
+
+def dev_gemm_w8b(a, w, bias, epilogue, out, rowpad=None, ln_rs=None, ln_c=None, diag=0, stream=None):
+    """Diag library only: the 8-wave bf16 GEMM (tools/diag/csrc/gemm_bf16_w8b.hip), EPI_STORE or
+    EPI_GELU_LN; all tensors contiguous on the device; diag 8 = no epilogue (timing only)."""
+    M, K = a.shape
+    N = w.shape[0]
+    call("vp_dev_gemm_w8b", epilogue, diag, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(rowpad),
+         _ptr(ln_rs), _ptr(ln_c), _stream(stream))
     return out
 
 
