@@ -238,45 +238,6 @@ def s3_ab(dev, g):
           flush=True)
 
 
-def pack_frag(w):
-    """W [N][K] -> the W-direct kernel's fragment order: per 128-column group and 32-deep k-chunk,
-    8 fragments (16 columns each) x 64 lanes x 8 bf16, lane = (k-octet within the chunk)*16 + column."""
-    N, K = w.shape
-    return w.view(N // 128, 8, 16, K // 32, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous().view(N, K)
-
-
-def wd_ab(dev, g):
-    """W-direct (W fragments straight from L2 into VGPRs, only A through LDS) vs the LDS-staged
-    kernel, EPI_BF16, at the forward's shapes: bitwise check, then interleaved timings with and
-    without the epilogue."""
-    for name, M, N, K, _ in SHAPES:
-        a, w, b = operands(M, N, K, g, dev)
-        wp = pack_frag(w)
-        o1 = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        o2 = torch.empty_like(o1)
-        nat.dev_gemm_kernel(4, a, w, b, 0, o1)
-        nat.dev_gemm_kernel(4, a, wp, b, 1000 + 7000, o2)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(o1, o2))
-        ref = (a.float() @ w.float().t()).to(torch.bfloat16)
-        err = (o2.float() - ref.float()).abs().max().item()
-        del ref
-        fns = {"lds": lambda: nat.dev_gemm_kernel(4, a, w, b, 0, o1),
-               "wd": lambda: nat.dev_gemm_kernel(4, a, wp, b, 1000 + 7000, o2),
-               "lds-noepi": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 8, o1),
-               "wd-noepi": lambda: nat.dev_gemm_kernel(4, a, wp, b, 1000 + 7008, o2),
-               "lds-nostage": lambda: nat.dev_gemm_kernel(4, a, w, b, 1000 + 12, o1),
-               "wd-nostage": lambda: nat.dev_gemm_kernel(4, a, wp, b, 1000 + 7012, o2)}
-        res = {k: [] for k in fns}
-        for _ in range(3):
-            for k, f in fns.items():
-                res[k].append(timeit(f, iters=10, warm=2))
-        flop = 2.0 * M * N * K
-        print(f"{name} wd==lds:{same} max|wd-fp32ref|={err:.3g}: " + " | ".join(
-            f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
-        del a, w, wp, o1, o2
-
-
 def w8b_ab(dev, g):
     """8-wave kernel with the 4-wave pipeline (gemm_bf16_w8b.hip) vs the 4-wave kernel: ffn_layer1's
     production epilogue (LN fold + GELU), the plain epilogue and no epilogue, at the forward's shapes."""
@@ -320,8 +281,6 @@ def main():
         grouped_pmc(dev, g)
     elif mode == "s3":
         s3_ab(dev, g)
-    elif mode == "wd":
-        wd_ab(dev, g)
     elif mode == "w8b":
         w8b_ab(dev, g)
     elif mode == "skew":

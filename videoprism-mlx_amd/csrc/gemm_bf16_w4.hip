@@ -86,19 +86,10 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // 7.78 -> 7.48 ms/step in the forward (tools/gemm_bench.py s3).  (Three A stages with all 16
 // pieces in h1 measured 468 vs 475 us isolated and nothing in the forward; the lead time alone is
 // not it -- spreading the pieces over both phases is.)
-// WD (W direct; diag builds only, measured 10-15 % slower than LDS-staged W):
-// W comes pre-packed in MFMA-fragment order (per 128-column group and 32-deep k-chunk, 8 fragments
-// x 64 lanes x 16 B = 8 KiB contiguous; tools/gemm_bench.py pack_frag) and each wave loads its
-// W fragments with buffer_load_dwordx4 straight into VGPRs -- one full-line 1 KiB request per
-// fragment, no LDS-DMA piece and no ds_read for W.  Only A goes through LDS (8 pieces and 8
-// ds_reads per K-tile and wave instead of 16 + 16).  W fragments of k-half (g, h1) are requested
-// at the start of h0(g), those of (g+1, h0) in h1(g) ahead of the A pieces, so h0 waits vmcnt(8)
-// (the A pieces stay in flight) and h1 vmcnt(0) as before.  Bitwise equal to the LDS form.
-template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false, bool WD = false>
+template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, int ngrp, EpiArgs ep) {
-  static_assert(!(WD && (S3 || PF)), "WD: 2-stage A staging only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tilesN = N / BN;
   const int T = (M / BM) * tilesN;
@@ -177,8 +168,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       coords(ld_tile, ld_tm, ld_tn);
     }
   };
-  // LDS: 2 x [A | W] K-tile buffers; S3: A buffers 0..2 then W buffers 0..1; WD: A buffers 0..1
-  auto a_buf = [&](int ai) { return smem + ai * ((S3 || WD) ? kOp : kBuf); };
+  // LDS: 2 x [A | W] K-tile buffers; S3: A buffers 0..2 then W buffers 0..1
+  auto a_buf = [&](int ai) { return smem + ai * (S3 ? kOp : kBuf); };
   auto w_buf = [&](int wi) { return smem + (S3 ? 3 * kOp + wi * kOp : wi * kBuf + kOp); };
   // p: 0..7 A pieces into A buffer `buf`, 8..15 W pieces into W buffer `buf`
   auto stage_piece = [&](int buf, int p) {
@@ -213,19 +204,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     else fw[set][q - 8] = *reinterpret_cast<const bf16x8*>(w_buf(wb) + woff[set] + (q - 8) * 2048);
   };
 
-  // WD: the 8 W fragments of this wave's 128 columns (group tn*2 + wn), k-chunk kc (32 deep) of
-  // the packed W: 8 KiB contiguous, fragment nt at +nt KiB, lane at +16*lane
-  const uint32_t wd_voff = (uint32_t)lane * 16;
-  auto wload = [&](int set, int tn, int kc) {
-    const int base = (((tn * 2 + wn) * (K >> 5) + kc) << 13);
-#pragma unroll
-    for (int nt = 0; nt < 8; ++nt) {
-      typedef unsigned wd_u32x4 __attribute__((ext_vector_type(4)));
-      const wd_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsW, (int)wd_voff, base + nt * 1024, 0);
-      fw[set][nt] = __builtin_bit_cast(bf16x8, v);
-    }
-  };
-
   f32x4 acc[8][8];
   // the first k-half of every tile starts its accumulators from 0 (C = inline constant)
   auto mfma = [&](int set, int idx, bool zero) {  // idx = nt*8 + mt
@@ -235,35 +213,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   };
 
   // ---- prologue: K-tiles 0, 1 into buffers 0, 1; fragments of (0, h0)
-  if constexpr (WD) {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) stage_piece(0, p);
-    wload(0, ld_tn, 0);
-    sched_fence();
-    advance();
+  for (int p = 0; p < 16; ++p) stage_piece(0, p);
+  advance();
 #pragma unroll
-    for (int p = 0; p < 8; ++p) stage_piece(1, p);
-    advance();
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    sched_fence();
-    __builtin_amdgcn_s_barrier();
-    sched_fence();
+  for (int p = 0; p < 16; ++p) stage_piece(1, p);
+  advance();
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  sched_fence();
+  __builtin_amdgcn_s_barrier();
+  sched_fence();
 #pragma unroll
-    for (int q = 0; q < 8; ++q) rd(0, 0, 0, q);
-  } else {
-#pragma unroll
-    for (int p = 0; p < 16; ++p) stage_piece(0, p);
-    advance();
-#pragma unroll
-    for (int p = 0; p < 16; ++p) stage_piece(1, p);
-    advance();
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    sched_fence();
-    __builtin_amdgcn_s_barrier();
-    sched_fence();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) rd(0, 0, 0, q);
-  }
+  for (int q = 0; q < 16; ++q) rd(0, 0, 0, q);
   int a3 = 0;  // S3: A buffer of the K-tile being computed (g % 3)
 
   uint32_t pf_dummy = 0;  // PF: destination of the L2-prefetch loads (never read)
@@ -355,78 +316,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     advance();  // after the scheduled block: its branch must not split it
   };
 
-  // WD K-tile g (A buffer cb, W tile column tn, K-tile kt): h0 = MFMAs on set 0; reads of A set 1
-  // <- (g, h1); W set 1 <- (g, h1) from global
-  auto h0w = [&](int cb, bool zero, int tn, int kt) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // W set 0 landed; A pieces of g+1 in flight
-    sched_fence();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) rd(1, cb, cb, q);
-    wload(1, tn, 2 * kt + 1);
-#pragma unroll
-    for (int idx = 0; idx < 64; ++idx) mfma(0, idx, zero);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-    }
-    sched_fence();
-  };
-  // h1: MFMAs on set 1; W set 0 <- (g+1, h0) (tile column ntn, K-tile nkt), then reads of A set 0
-  // <- (g+1, h0) and the 8 A pieces of K-tile g+2 into buffer cb -- the W loads strictly before the
-  // pieces (separate scheduling regions), so the next h0's vmcnt(8) leaves only the pieces
-  auto h1w = [&](int cb, int ntn, int nkt) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    sched_fence();
-    mfma(1, 0, false);
-    mfma(1, 1, false);
-    sched_fence();
-    __builtin_amdgcn_s_barrier();
-    sched_fence();
-    wload(0, ntn, 2 * nkt);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) rd(0, cb ^ 1, cb ^ 1, q);
-#pragma unroll
-    for (int idx = 2; idx < 32; ++idx) mfma(1, idx, false);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    sched_fence();
-#pragma unroll
-    for (int q = 4; q < 8; ++q) rd(0, cb ^ 1, cb ^ 1, q);
-    if constexpr (!(DIAG & 4)) {
-#pragma unroll
-      for (int p = 0; p < 8; ++p) stage_piece(cb, p);
-    }
-#pragma unroll
-    for (int idx = 32; idx < 64; ++idx) mfma(1, idx, false);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
-    }
-    sched_fence();
-    advance();
-  };
-
   int g = 0;
   if constexpr (DIAG & 64) {
     // ep.pos_rows (unused by EPI_BF16) = groups * 10000 + delay per group in 10-ns ticks
@@ -472,28 +361,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
             rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
-    if constexpr (WD) {
-      // W tile column of this tile and of the next one (the last K-tile's h1 requests the next
-      // tile's first W fragments; past the last tile it re-requests this tile's, never used)
-      int jtm, jtn, ntm, ntn;
-      coords(first + j * stride, jtm, jtn);
-      if (j + 1 < count) coords(first + (j + 1) * stride, ntm, ntn);
-      else ntn = jtn;
-      h0w(g & 1, true, jtn, 0);
-      h1w(g & 1, nk > 1 ? jtn : ntn, nk > 1 ? 1 : 0);
-      ++g;
-      for (int kt = 1; kt < nk; ++kt, ++g) {
-        h0w(g & 1, false, jtn, kt);
-        h1w(g & 1, kt + 1 < nk ? jtn : ntn, kt + 1 < nk ? kt + 1 : 0);
-      }
-    } else {
-      h0(g & 1, true);
-      h1(g & 1, (DIAG & 16) && j > 0);
-      ++g;
-      for (int kt = 1; kt < nk; ++kt, ++g) {
-        h0(g & 1, false);
-        h1(g & 1, false);
-      }
+    h0(g & 1, true);
+    h1(g & 1, (DIAG & 16) && j > 0);
+    ++g;
+    for (int kt = 1; kt < nk; ++kt, ++g) {
+      h0(g & 1, false);
+      h1(g & 1, false);
     }
 
     // ---- epilogue of tile j.  acc[nt][mt] holds D[row mb + 16*mt][cols nb + 16*nt + 4*(lane>>4)
@@ -509,7 +382,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const int m0 = etm * BM + wm * 128, n0 = etn * BN + wn * 128;
     using Tr = EpiTraits<EPI>;
     // S3: the A buffer of the tile's last K-tile (free since its h1 barrier; refilled in the next h0)
-    char* scr = (S3 ? a_buf(a3 == 0 ? 2 : a3 - 1) : WD ? smem + 2 * kOp : smem + kLds) + w * kScr;
+    char* scr = (S3 ? a_buf(a3 == 0 ? 2 : a3 - 1) : smem + kLds) + w * kScr;
     if constexpr (Tr::kQkAttn || Tr::kVAttn) {
       // ---- fused temporal attention (EPI_QK_TATTN_LN / EPI_V_TATTN_LN, see vp_kernels.h).  A
       // 16-row block mt of this wave's 128 rows is one (b n) sequence of T = 16 frames; the
@@ -771,12 +644,12 @@ int num_cus_w4() {
   return n;
 }
 
-template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false, bool WD = false>
+template <int EPI, int DIAG = 0, int PF = 0, bool S3 = false>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG, PF, S3, WD>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -785,8 +658,8 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
   // DIAG 32768: ungrouped, 65536: XCD-pair split of W (A/B; needs (M/BM) % 4 == 0, (N/BN) even, grid % 8 == 0)
   const int ngrp = (DIAG & 32768) ? N / BN : (DIAG & 65536) ? -1 : w4_ngrp(M, N, K, grid);
-  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3, WD>));
-  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3, WD>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
+  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>));
+  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, DIAG, PF, S3>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda, W,
                      ldw, M, N, K, ngrp, ep);
   return hipGetLastError();
 }
@@ -897,12 +770,6 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       case 2009: return launch_w4<EPI_GELU_BF16_LN, 0>(A, lda, W, ldw, M, N, K, ep, s);
       // + scalar (unpacked) GELU arithmetic
       case 2010: return launch_w4<EPI_GELU_BF16_LN, 512 | 1024>(A, lda, W, ldw, M, N, K, ep, s);
-      // W-direct builds (W pre-packed in fragment order, tools/gemm_bench.py pack_frag): plain / no
-      // epilogue / no A staging -- measured slower than the LDS-staged W
-      case 7000: return launch_w4<EPI_BF16, 0, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-      case 7008: return launch_w4<EPI_BF16, 8, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-      case 7004: return launch_w4<EPI_BF16, 4, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
-      case 7012: return launch_w4<EPI_BF16, 12, 0, false, true>(A, lda, W, ldw, M, N, K, ep, s);
     }
     return hipErrorInvalidValue;
   }
