@@ -41,3 +41,22 @@ def test_bench_json_contract(cuda):
         rec = json.load(f)
     if rec.get("src_hash") == _native.source_fingerprint():
         assert rf["traffic"] is not None and rf["traffic"] > 0, rf
+
+
+def test_bench_under_torchrun_world1(cuda):
+    """The driver's N > 1 launch form (torch.distributed.run, rendezvous on 127.0.0.1) at one rank: the
+    launcher-provided RANK / WORLD_SIZE path of bench.py (gloo group for the barrier and the max over
+    ranks) prints the same contract line."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-profile"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0 and d["config"]["parallelism"].startswith("dp1")
