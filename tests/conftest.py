@@ -5,7 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "videoprism-mlx_amd")
-for p in (ROOT, PKG_DIR, os.path.join(ROOT, "tests")):
+for p in (ROOT, PKG_DIR, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tools")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

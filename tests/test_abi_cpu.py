@@ -30,10 +30,17 @@ def test_product_library_has_no_ablation_builds():
     """The A/B and ablation kernels live in the tools' diag library only (make diag): the product
     library exports no diag entry points and reads no kernel-selection environment switch."""
     lib = ctypes.CDLL(_native.library_path())
-    for sym in ("vp_dev_gemm_diag", "vp_dev_attention_diag"):
+    for sym in ("vp_dev_gemm_diag", "vp_dev_attention_diag", "vp_dev_gemm_w4_abl", "vp_dev_gemm_ov",
+                "vp_dev_gemm_w8b", "vp_dev_qkv_attention"):
         assert not hasattr(lib, sym), sym
     blob = open(_native.library_path(), "rb").read()
-    assert b"VP_GEMM_KERNEL" not in blob and b"gemm_bf16_ov" not in blob
+    assert b"VP_GEMM_KERNEL" not in blob and b"gemm_bf16_ov" not in blob and b"VP_NO_TATTN" not in blob
+    assert b"gemm_bf16_w8b" not in blob and b"qkv_attn_spatial" not in blob
+    # every 4-wave GEMM kernel in the product library is an ABL = 0 (production) instantiation
+    import check_kernels
+    names = [k[".name"] for k in check_kernels.kernels(_native.library_path())]
+    w4 = [n for n in names if "gemm_bf16_w4_kernel" in n]
+    assert w4 and all(n.endswith("ELi0EEEvPKtlS3_liiiiNS_7EpiArgsE") for n in w4), w4
 
 
 def test_comm_entry_points_without_a_gpu():

@@ -1,5 +1,5 @@
 """A/B equality checks of the tools' diag library (VP_DIAG_LIB=1; `make -C videoprism-mlx_amd diag`):
-the overlapped-epilogue GEMM (gemm_bf16_ov) and the spatial-attention layout variants must be
+the overlapped-epilogue GEMM (gemm_bf16_ov) and the 8-wave GEMM with the 4-wave pipeline must be
 bitwise equal to the production kernels.  Not part of tests/: the product library carries none of
 these builds.  Run on the GPU box:  VP_DIAG_LIB=1 python tools/ab_tests.py"""
 import os
@@ -28,26 +28,14 @@ def ov_vs_w4(M=16384, N=2304, K=768):
         outs = {}
         for which in (4, 2):
             o = x0.clone() if epi == nat.EPI_RESID_BF16 else torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-            nat.dev_gemm_kernel(which, a, w, b, epi, o, resid=o if epi == nat.EPI_RESID_BF16 else None)
+            r = o if epi == nat.EPI_RESID_BF16 else None
+            if which == 4:
+                nat.dev_gemm_kernel(4, a, w, b, epi, o, resid=r)
+            else:
+                nat.dev_gemm_ov(a, w, b, epi, o, resid=r)
             outs[which] = o
         torch.cuda.synchronize()
         print(f"ov vs w4 epi {epi}: bitwise {torch.equal(outs[2], outs[4])}")
-
-
-def attention_variants():
-    from test_gpu_kernels import _qkv
-    nseq, heads, S = 3, 12, 256
-    qkv = _bf(_qkv(nseq, S, heads, 5)).cuda()
-    ref = nat.op_attention(qkv, nseq, S, heads, 50.0)
-    for variant in (16, 32, 48):
-        src = qkv
-        if variant & 16:  # [M, 3, heads, 64] -> [3, heads, M, 64]
-            src = qkv.reshape(nseq * S, 3, heads, 64).permute(1, 2, 0, 3).contiguous()
-        out = torch.empty_like(ref)
-        nat.call("vp_dev_attention_diag", variant, src.data_ptr(), out.data_ptr(), nseq, heads, 50.0,
-                 torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        print(f"attention variant {variant}: bitwise {torch.equal(out, ref)}")
 
 
 def w8b_vs_w4():
@@ -76,4 +64,3 @@ def w8b_vs_w4():
 if __name__ == "__main__":
     w8b_vs_w4()
     ov_vs_w4()
-    attention_variants()

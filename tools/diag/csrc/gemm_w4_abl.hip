@@ -1,0 +1,23 @@
+// Ablation builds of the product 4-wave GEMM (videoprism-mlx_amd/csrc/gemm_w4_kernel.h) for the
+// tools' diag library only: the same template with parts of the pipeline switched off, to price
+// them (tools/gemm_bench.py ablate).  Results are garbage.
+#include "gemm_w4_kernel.h"
+#include "vp_diag.h"
+
+namespace vp {
+
+hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                            int N, int K, const EpiArgs& ep, hipStream_t s) {
+  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
+#define VP_ABL(S3, X) \
+  case X: return launch_w4<EPI_BF16, false, S3, X>(A, lda, W, ldw, M, N, K, ep, s);
+  if (s3) {
+    switch (abl) { VP_ABL(true, 0) VP_ABL(true, 2) VP_ABL(true, 4) VP_ABL(true, 6) VP_ABL(true, 8) VP_ABL(true, 14) }
+  } else {
+    switch (abl) { VP_ABL(false, 0) VP_ABL(false, 2) VP_ABL(false, 4) VP_ABL(false, 6) VP_ABL(false, 8) VP_ABL(false, 14) }
+  }
+#undef VP_ABL
+  return hipErrorInvalidValue;
+}
+
+}  // namespace vp

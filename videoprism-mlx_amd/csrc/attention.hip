@@ -17,7 +17,6 @@
 // attention_temporal_bf16: S = T <= 16 frames.  One wave per (sequence, head), 16x16x32 for
 //   Q.K^T and 16x16x16 for P.V; memory-bound on the qkv rows.
 // attention_f32: generic fp32 path (fprop_dtype=float32), online softmax, exact tanhf/expf.
-#include <cstdlib>
 #include <type_traits>
 
 #include "vp_common.h"
@@ -39,8 +38,6 @@ __device__ __forceinline__ float capped_exp(float x, float two_log2e_over_cap, f
 __device__ __forceinline__ int swzK(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swzV(int row) { return ((row >> 1) & 1) << 2; }
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
 __device__ __forceinline__ bf16x4 tr_read(const char* p) {
   s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) s16x4*)(p));
@@ -54,14 +51,13 @@ constexpr int kSpS = 256;
 constexpr int kSpThreads = 512;
 constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 
-// DIAG (ablation builds, results garbage): 1 = no capped-exp VALU (p = logit), 2 = no P.V MFMAs
 // q|k|v layout by strides (elements): row rs, head hs, section (q -> k -> v) sec; the row-major
-// fused projection output is (3D, 64, D), a head-major one (64, M*64, heads*M*64).
-// STAGE: O goes through LDS and leaves as whole 128-B row segments (8 rows per store).
-template <bool MASK, int DIAG = 0, bool STAGE = false>
+// fused projection output is (3D, 64, D).  O goes through LDS and leaves as whole 128-B row
+// segments (8 rows per store).
+template <bool MASK>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
-    const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec, CapPoly cp) {
+    const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + kSpS * 128;
@@ -80,24 +76,16 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * hs;
 
   // ---- this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j),
-  // requested first by loads the compiler does not see (a visible load would make hipcc wait
-  // vmcnt(0) at its first use and drain the K/V stream below); retired by the chunk-0 wait ----
+  // requested ahead of the K/V stream.  hipcc cannot count a plain load against the LDS-DMA
+  // pieces behind it (mixed event kinds: it emits vmcnt(0), draining the stream before the first
+  // key tile), so these are asm loads retired by chunk 0's wait statement, which names qf as
+  // operands (cdna_hip_programming.md §5.7 item 1, form (ii)); tools/check_kernels.py audits the
+  // assembly for any compiler access to those registers in between, and the build refuses
+  // scratch or spills in every product kernel ----
   const int q0 = w * 32;
   const int half = lane >> 5;
   bf16x8 qf[4];
-  if constexpr ((DIAG & 64) != 0) {  // ablation: no Q loads
-#pragma unroll
-    for (int kd = 0; kd < 4; ++kd) {
-      qf[kd] = bf16x8{};
-      asm volatile("" : "+v"(qf[kd]));
-    }
-  } else if constexpr ((DIAG & 8) != 0) {  // ablation: Q by whole 128-B lines (8 rows per load)
-#pragma unroll
-    for (int kd = 0; kd < 4; ++kd) {
-      const bf16_t* qp = base + (int64_t)(q0 + kd * 8 + (lane >> 3)) * ld + 8 * (lane & 7);
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qp));
-    }
-  } else {
+  {
     const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
 #pragma unroll
     for (int kd = 0; kd < 4; ++kd)
@@ -114,13 +102,12 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       const int row = (piece & 31) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
       const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * sec : sec) + c * 8;
-      if constexpr ((DIAG & 128) == 0)  // ablation 128: no K/V staging
-        __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
     }
   if constexpr (MASK) {  // (padded batches: no streaming)
     if (threadIdx.x < kSpS) kp[threadIdx.x] = key_pad[(int64_t)seq * kSpS + threadIdx.x];
     if (threadIdx.x == 0) *allmask = 1;
-    wait_vmcnt0();
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) : : "memory");
     __syncthreads();
   }
   // chunk cc of every wave has landed: this wave's vmcnt leaves only its younger chunks in
@@ -128,11 +115,10 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   auto chunk_ready = [&](auto CC) {
     constexpr int cc = decltype(CC)::value;
     if constexpr (!MASK) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (3 - cc)) : "memory");
-      if constexpr (cc == 0) {
-#pragma unroll
-        for (int kd = 0; kd < 4; ++kd) asm volatile("" : "+v"(qf[kd]));
-      }
+      if constexpr (cc == 0)  // also retires the Q loads (issued before every piece)
+        asm volatile("s_waitcnt vmcnt(6)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) : : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (3 - cc)) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -168,16 +154,12 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   };
   // numerators of tile kt, then O^T += V^T . X
   auto pv = [&](int kt, const f32x16& x) {
-    // numerators: register i <-> key kt*32 + (i&3) + 8(i>>2) + 4*half
+    // numerators: register i <-> key kt*32 + (i&3) + 8(i>>2) + 4*half (exact three-transcendental
+    // form: the one-transcendental polynomial moved the full-depth LvT-B bf16 embedding across the
+    // 1e-3 bar)
     float p[16];
-    // DIAG 4: the one-transcendental numerator of capped_exp16 (A/B build; production keeps the
-    // exact form -- the polynomial moved the full-depth LvT-B bf16 embedding across the 1e-3 bar)
-    if constexpr ((DIAG & 4) != 0) {
-      capped_exp16(x, p, c1, c2, cp);
-    } else {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) p[i] = (DIAG & 1) ? x[i] : capped_exp(x[i], c1, c2);
-    }
+    for (int i = 0; i < 16; ++i) p[i] = capped_exp(x[i], c1, c2);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float e = p[i];
@@ -196,10 +178,13 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       for (int j = 0; j < 4; ++j) u[j] = pack_bf16x2(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
       pf[s] = *reinterpret_cast<bf16x8*>(u);
     }
-    // O^T += V^T . X  (A = V^T via transposed reads, B = P^T numerators).  The transposed reads
-    // are inline asm: hipcc puts a vmcnt(0) for the in-flight K/V chunks in front of a visible
-    // ds_read_tr (it cannot tell it from a read of a chunk still landing); lgkmcnt(0) retires them
-    s16x4 vr[2][2][2];
+    // O^T += V^T . X  (A = V^T via transposed reads, B = P^T numerators).  hipcc puts a vmcnt(0)
+    // for the in-flight K/V chunks in front of a visible ds_read_tr (it cannot tell it from a read
+    // of a chunk still landing), so the 8 reads are inline asm -- issued together with their
+    // lgkmcnt(0) in ONE statement with early-clobber outputs: the destinations are defined only
+    // once the data has landed, so no compiler copy or spill can touch them in flight
+    // (cdna_hip_programming.md §5.7 item 1, form (i))
+    uint32_t ad[2][2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int key = kt * 32 + 16 * s + 4 * half + trq;
@@ -207,18 +192,11 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       for (int dh = 0; dh < 2; ++dh) {
         const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
         const int c = col >> 3;
-        const uint32_t ad = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2);
-        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[s][dh][0]) : "v"(ad));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(vr[s][dh][1]) : "v"(ad));
+        ad[s][dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2);
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
-        asm volatile("" : "+v"(vr[s][dh][0]), "+v"(vr[s][dh][1]));
-      }
+    s16x4 vr[2][2][2];
+    lds_tr_read8(vr, ad);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -226,13 +204,8 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       for (int dh = 0; dh < 2; ++dh) {
         const s16x4 lo = vr[s][dh][0], hi = vr[s][dh][1];
         const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if constexpr (DIAG & 2) {
-          asm volatile("" ::"v"(vf), "v"(pf[s]));
-        } else if (dh == 0) {
-          y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y0, 0, 0, 0);
-        } else {
-          y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y1, 0, 0, 0);
-        }
+        if (dh == 0) y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y0, 0, 0, 0);
+        else y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y1, 0, 0, 0);
       }
     }
   };
@@ -251,41 +224,28 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   }
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;
-  // y_dh[i] = O^T[d = 32dh + (i&3) + 8(i>>2) + 4*half][q = q0 + (l&31)]
-  if constexpr (STAGE) {
-    // every wave is done with K/V: the wave's 32 x 64 output tile goes to its 4 KiB of the K
-    // region ([q][16-B chunk ^ (q & 7)]), then 8 lanes per row store whole 128-B segments
-    __syncthreads();
-    char* st = smem + w * 4096;
-    const int ql = lane & 31;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const uint2 v0 = make_uint2(pack_bf16x2(y0[4 * g4] * inv, y0[4 * g4 + 1] * inv),
-                                  pack_bf16x2(y0[4 * g4 + 2] * inv, y0[4 * g4 + 3] * inv));
-      const uint2 v1 = make_uint2(pack_bf16x2(y1[4 * g4] * inv, y1[4 * g4 + 1] * inv),
-                                  pack_bf16x2(y1[4 * g4 + 2] * inv, y1[4 * g4 + 3] * inv));
-      *reinterpret_cast<uint2*>(st + ql * 128 + (((g4) ^ (ql & 7)) << 4) + 8 * half) = v0;
-      *reinterpret_cast<uint2*>(st + ql * 128 + (((4 + g4) ^ (ql & 7)) << 4) + 8 * half) = v1;
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int r = p * 8 + (lane >> 3), c = lane & 7;
-      const uint4 v = *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
-      *reinterpret_cast<uint4*>(o + ((int64_t)seq * kSpS + q0 + r) * D + h * 64 + c * 8) = v;
-    }
-    return;
-  }
-  bf16_t* op = o + ((int64_t)seq * kSpS + q0 + (lane & 31)) * D + h * 64 + 4 * half;
+  // y_dh[i] = O^T[d = 32dh + (i&3) + 8(i>>2) + 4*half][q = q0 + (l&31)].  Every wave is done with
+  // K/V: the wave's 32 x 64 output tile goes to its 4 KiB of the K region ([q][16-B chunk ^ (q & 7)]),
+  // then 8 lanes per row store whole 128-B segments
+  __syncthreads();
+  char* st = smem + w * 4096;
+  const int ql = lane & 31;
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
-    uint2 v0 = make_uint2(pack_bf16x2(y0[4 * g4] * inv, y0[4 * g4 + 1] * inv),
-                          pack_bf16x2(y0[4 * g4 + 2] * inv, y0[4 * g4 + 3] * inv));
-    uint2 v1 = make_uint2(pack_bf16x2(y1[4 * g4] * inv, y1[4 * g4 + 1] * inv),
-                          pack_bf16x2(y1[4 * g4 + 2] * inv, y1[4 * g4 + 3] * inv));
-    *reinterpret_cast<uint2*>(op + 8 * g4) = v0;
-    *reinterpret_cast<uint2*>(op + 32 + 8 * g4) = v1;
+    const uint2 v0 = make_uint2(pack_bf16x2(y0[4 * g4] * inv, y0[4 * g4 + 1] * inv),
+                                pack_bf16x2(y0[4 * g4 + 2] * inv, y0[4 * g4 + 3] * inv));
+    const uint2 v1 = make_uint2(pack_bf16x2(y1[4 * g4] * inv, y1[4 * g4 + 1] * inv),
+                                pack_bf16x2(y1[4 * g4 + 2] * inv, y1[4 * g4 + 3] * inv));
+    *reinterpret_cast<uint2*>(st + ql * 128 + (((g4) ^ (ql & 7)) << 4) + 8 * half) = v0;
+    *reinterpret_cast<uint2*>(st + ql * 128 + (((4 + g4) ^ (ql & 7)) << 4) + 8 * half) = v1;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = p * 8 + (lane >> 3), c = lane & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
+    *reinterpret_cast<uint4*>(o + ((int64_t)seq * kSpS + q0 + r) * D + h * 64 + c * 8) = v;
   }
 }
 
@@ -463,7 +423,7 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   if (!(cap > 0.0f)) return hipErrorInvalidValue;
   static bool attr[2] = {false, false};
   const int mi = key_pad ? 1 : 0;
-  const void* fn = key_pad ? (const void*)attn_spatial_kernel<true, 0, true> : (const void*)attn_spatial_kernel<false, 0, true>;
+  const void* fn = key_pad ? (const void*)attn_spatial_kernel<true> : (const void*)attn_spatial_kernel<false>;
   if (!attr[mi]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
     if (e != hipSuccess) return e;
@@ -476,57 +436,18 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   // (a persistent variant -- one workgroup per CU walking (frame, head) pairs, next pair's
   // Q/K/V staged by LDS-DMA during the current one, 160 KiB LDS -- measured 255 vs 218 us: at
   // 2 waves per SIMD the softmax/P.V phase loses more than the continuous stream gains)
-  // O leaves through LDS as whole 128-B row segments (tools/attn_bench.py: 217 -> 209 us at the
-  // bench shape); a head-major q|k|v layout measured only 1 % faster and is not used
+  // O leaves through LDS as whole 128-B row segments (217 -> 209 us at the bench shape); a
+  // head-major q|k|v layout measured only 1 % faster and is not used
   const int64_t D = heads * 64;
   VP_NOTE_KERNEL(fn);
   if (key_pad)
-    hipLaunchKernelGGL((attn_spatial_kernel<true, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
-                       key_pad, rev, 3 * D, (int64_t)64, D, make_cap_poly(cap));
+    hipLaunchKernelGGL(attn_spatial_kernel<true>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad,
+                       rev, 3 * D, (int64_t)64, D);
   else
-    hipLaunchKernelGGL((attn_spatial_kernel<false, 0, true>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap,
-                       key_pad, rev, 3 * D, (int64_t)64, D, make_cap_poly(cap));
+    hipLaunchKernelGGL(attn_spatial_kernel<false>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad,
+                       rev, 3 * D, (int64_t)64, D);
   return hipGetLastError();
 }
-
-#ifdef VP_DIAG
-hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
-                                  float cap, hipStream_t s) {
-  const dim3 grid(num_seq * heads);
-  const int64_t D = heads * 64, M = (int64_t)num_seq * kSpS;
-  // diag >= 16: layout / store variants of the production kernel (bit 16: head-major q|k|v,
-  // bit 32: LDS-staged O stores)
-  const int64_t rs = (diag & 16) ? 64 : 3 * D, hs = (diag & 16) ? M * 64 : 64, sec = (diag & 16) ? heads * M * 64 : D;
-  auto go = [&](const void* fn, auto kern) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, nullptr, 0, rs, hs, sec,
-                       make_cap_poly(cap));
-    return hipGetLastError();
-  };
-  if (diag == 4 + 32)  // staged stores + polynomial numerator
-    return go((const void*)attn_spatial_kernel<false, 4, true>, attn_spatial_kernel<false, 4, true>);
-  if (diag >= 16 && diag < 1000) {
-    if (diag & 32) return go((const void*)attn_spatial_kernel<false, 0, true>, attn_spatial_kernel<false, 0, true>);
-    return go((const void*)attn_spatial_kernel<false, 0, false>, attn_spatial_kernel<false, 0, false>);
-  }
-  switch (diag) {
-    // memory-pattern ablations on the production (staged-store) build: 8 = Q by whole lines,
-    // 64 = no Q loads, 128 = no K/V staging; | 3 = no numerators, no P.V
-    case 1000 + 3: return go((const void*)attn_spatial_kernel<false, 3, true>, attn_spatial_kernel<false, 3, true>);
-    case 1000 + 8: return go((const void*)attn_spatial_kernel<false, 8, true>, attn_spatial_kernel<false, 8, true>);
-    case 1000 + 11: return go((const void*)attn_spatial_kernel<false, 11, true>, attn_spatial_kernel<false, 11, true>);
-    case 1000 + 67: return go((const void*)attn_spatial_kernel<false, 67, true>, attn_spatial_kernel<false, 67, true>);
-    case 1000 + 131: return go((const void*)attn_spatial_kernel<false, 131, true>, attn_spatial_kernel<false, 131, true>);
-    case 1000 + 195: return go((const void*)attn_spatial_kernel<false, 195, true>, attn_spatial_kernel<false, 195, true>);
-    case 0: return go((const void*)attn_spatial_kernel<false, 0>, attn_spatial_kernel<false, 0>);
-    case 1: return go((const void*)attn_spatial_kernel<false, 1>, attn_spatial_kernel<false, 1>);
-    case 2: return go((const void*)attn_spatial_kernel<false, 2>, attn_spatial_kernel<false, 2>);
-    case 3: return go((const void*)attn_spatial_kernel<false, 3>, attn_spatial_kernel<false, 3>);
-  }
-  return hipErrorInvalidValue;
-}
-#endif
 
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s) {

@@ -36,8 +36,6 @@ __device__ __forceinline__ float capped_exp(float x, float two_log2e_over_cap, f
 __device__ __forceinline__ int swzK(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swzV(int row) { return ((row >> 1) & 1) << 2; }
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
 constexpr int kLgThreads = 512;          // 8 waves x 32 queries
 constexpr int kLgQ = 256;                // queries per workgroup
 constexpr int kLgChunk = 64;             // keys per LDS stage
@@ -66,8 +64,10 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
   const int q0 = qb * kLgQ + w * 32;
   const int half = lane >> 5;
 
-  // this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j); loads
-  // the compiler does not see, retired by the first chunk wait
+  // this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j): asm loads
+  // (hipcc cannot count a plain load against the LDS-DMA pieces behind it and would drain the
+  // stream with vmcnt(0)), retired by the prologue's wait statement that names qf (form (ii) of
+  // cdna_hip_programming.md §5.7 item 1; audited by tools/check_kernels.py)
   bf16x8 qf[4];
   {
     const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
@@ -90,8 +90,10 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
     }
   };
 #pragma unroll
-  for (int c = 0; c < kLgStages - 1; ++c)
-    if (c < nchunks) issue(c);
+  for (int c = 0; c < kLgStages - 1; ++c) issue(c);  // nchunks >= 4 (S % 256 == 0, checked by the launcher)
+  // Q and chunk 0 landed (chunks 1, 2 -- 4 pieces -- may still be in flight); the loop's own
+  // chunk-0 wait is then a no-op
+  asm volatile("s_waitcnt vmcnt(4)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) : : "memory");
 
   const float c1 = 2.0f * kLog2e / cap;
   const float c2 = cap * kLog2e;
@@ -111,10 +113,6 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
     if (younger >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (c == 0) {
-#pragma unroll
-      for (int kd = 0; kd < 4; ++kd) asm volatile("" : "+v"(qf[kd]));
-    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -125,19 +123,18 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
     for (int kt = 0; kt < kLgChunk / 32; ++kt) {
       f32x16 x = {};
       const int krow = kt * 32 + krow_l;
+      // K and V reads: inline asm (a visible LDS read would get a vmcnt(0) for the chunks still
+      // landing), reads and wait in one statement (vp_common.h lds_read4_b128 / lds_tr_read8)
       bf16x8 kf[4];
+      uint32_t kad[4];
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) {
         const int cc = 2 * kd + half;
-        const uint32_t ad = (uint32_t)(uintptr_t)VP_LDS_PTR(Ks + krow * 128 + ((cc ^ swzK(krow)) << 4));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(kf[kd]) : "v"(ad));
+        kad[kd] = (uint32_t)(uintptr_t)VP_LDS_PTR(Ks + krow * 128 + ((cc ^ swzK(krow)) << 4));
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_read4_b128(kf, kad);
 #pragma unroll
-      for (int kd = 0; kd < 4; ++kd) {
-        asm volatile("" : "+v"(kf[kd]));
-        x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
-      }
+      for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
       capped_exp16(x, p, c1, c2, cp);
 #pragma unroll
@@ -150,7 +147,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
         for (int j = 0; j < 4; ++j) u[j] = pack_bf16x2(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
         pf[s] = *reinterpret_cast<bf16x8*>(u);
       }
-      s16x4 vr[2][2][2];
+      uint32_t vad[2][2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int key = kt * 32 + 16 * s + 4 * half + trq;
@@ -158,17 +155,11 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
         for (int dh = 0; dh < 2; ++dh) {
           const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
           const int cc = col >> 3;
-          const uint32_t ad =
-              (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((cc ^ swzV(key)) << 4) + (col & 7) * 2);
-          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[s][dh][0]) : "v"(ad));
-          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(vr[s][dh][1]) : "v"(ad));
+          vad[s][dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((cc ^ swzV(key)) << 4) + (col & 7) * 2);
         }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh) asm volatile("" : "+v"(vr[s][dh][0]), "+v"(vr[s][dh][1]));
+      s16x4 vr[2][2][2];
+      lds_tr_read8(vr, vad);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {

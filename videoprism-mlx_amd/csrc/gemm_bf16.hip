@@ -57,11 +57,7 @@ __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0
 // W stay in that XCD's L2.  The K-tile stream is global over a workgroup's tiles: the
 // glds of the next tile's first K-tiles are issued during the last K-tiles of the current
 // one, and its epilogue runs while they are in flight (no per-tile pipeline drain).
-// DIAG (ablation builds for tools/gemm_bench.py only; results are garbage): 1 = no glds in
-// the K loop, 2 = no ds_reads in the K loop, 4 = no barriers in the K loop, 8 = glds issued
-// but no vmcnt wait in the K loop, 16 = register staging (global_load_dwordx4 two phases
-// ahead, ds_write_b128 when the region is free) instead of global_load_lds, 32 = no epilogue.
-template <int EPI, int DIAG = 0>
+template <int EPI>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, EpiArgs ep) {
@@ -111,7 +107,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     tn = tile - tm * tilesN;
   };
   auto stage = [&](int region, int g) {
-    if constexpr (DIAG & 1) { if (g > 1) return; }
     int tm, tn, kt;
     tile_of(g, tm, tn, kt);
     char* dst = smem + (g & 1) * kBuf + region * kRegion + w * 2048;
@@ -125,40 +120,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     __builtin_amdgcn_global_load_lds(VP_GLB_PTR(base + o1), VP_LDS_PTR(dst + 1024), 16, 0, 0);
   };
 
-  // ---- register staging (DIAG & 16): per-lane linear source chunk, swizzled LDS write ----
-  constexpr bool kReg = DIAG & 16;
-  bf16x8 stg[2][2];
-  int64_t roffA[2][2], roffB[2][2];
-  int wdst[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rl = (w * 2 + i) * 8 + (lane >> 3);
-    wdst[i] = rl * 128 + (((lane & 7) ^ swz(rl)) << 4);
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      roffA[qq][i] = (int64_t)(((rl >> 6) << 7) + qq * 64 + (rl & 63)) * lda + (lane & 7) * 8;
-      roffB[qq][i] = (int64_t)(((rl >> 5) << 6) + qq * 32 + (rl & 31)) * ldw + (lane & 7) * 8;
-    }
-  }
-  auto gload = [&](int region, int g, int slot) {
-    g = g < total ? g : total - 1;
-    int tm, tn, kt;
-    tile_of(g, tm, tn, kt);
-    const bf16_t* base = region < 2 ? A + (int64_t)tm * BM * lda + kt * BK
-                                    : W + (int64_t)tn * BN * ldw + kt * BK;
-    const int64_t o0 = region == RA0 ? roffA[0][0] : region == RA1 ? roffA[1][0]
-                     : region == RB0 ? roffB[0][0] : roffB[1][0];
-    const int64_t o1 = region == RA0 ? roffA[0][1] : region == RA1 ? roffA[1][1]
-                     : region == RB0 ? roffB[0][1] : roffB[1][1];
-    stg[slot][0] = *reinterpret_cast<const bf16x8*>(base + o0);
-    stg[slot][1] = *reinterpret_cast<const bf16x8*>(base + o1);
-  };
-  auto swrite = [&](int region, int g, int slot) {
-    char* dst = smem + (g & 1) * kBuf + region * kRegion;
-    *reinterpret_cast<bf16x8*>(dst + wdst[0]) = stg[slot][0];
-    *reinterpret_cast<bf16x8*>(dst + wdst[1]) = stg[slot][1];
-  };
-
   f32x4 acc[4][8];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -170,14 +131,12 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   const int brow = wn * 32 + l16;   // local row inside a B region
   bf16x8 af[8], bf[4];
   auto read_A = [&](const char* reg) {
-    if constexpr (DIAG & 2) { asm volatile("" : "+v"(af[0]), "+v"(af[5])); return; }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) af[kk * 4 + mt] = lds_frag(reg, arow + mt * 16, kk * 4 + cq);
   };
   auto read_B = [&](const char* reg) {
-    if constexpr (DIAG & 2) { asm volatile("" : "+v"(bf[0]), "+v"(bf[3])); return; }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -198,7 +157,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   auto barrier = [] {
     sched_fence();
-    if constexpr (!(DIAG & 4)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     sched_fence();
   };
 
@@ -207,20 +166,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   // Every region is restaged >= 2 phases after its last ds_read (so reads need not be
   // retired before the barrier), and P4's counted vmcnt(4) leaves only the two newest
   // half-tiles in flight: all of K-tile g+1 has landed before the barrier into P1(g+1).
-  if constexpr (kReg) {
-    // prologue: K-tile 0 and A0/B1 of K-tile 1 written directly; A1(1) -> slot 0, B0(1) -> slot 1
-    const int pro[6][2] = {{RA0, 0}, {RB0, 0}, {RB1, 0}, {RA1, 0}, {RA0, 1}, {RB1, 1}};
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      gload(pro[i][0], pro[i][1], 0);
-      swrite(pro[i][0], pro[i][1] < total ? pro[i][1] : 0, 0);
-    }
-    gload(RA1, 1, 0);
-    gload(RB0, 1, 1);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the prologue ds_writes
-    barrier();
-    if (wm == 1) barrier();
-  } else {
   stage(RA0, 0); stage(RB0, 0); stage(RB1, 0); stage(RA1, 0);
   if (total > 1) {
     stage(RA0, 1); stage(RB1, 1);
@@ -230,7 +175,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   }
   barrier();
   if (wm == 1) barrier();  // stagger: waves 4-7 run one barrier behind
-  }
 
   int kt = 0, j = 0;
   for (int g = 0; g < total; ++g) {
@@ -239,49 +183,32 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     // P1: quadrant (0,0)
     read_A(cur + RA0 * kRegion);
     read_B(cur + RB0 * kRegion);
-    if constexpr (kReg) {  // write A1(g+1) (loaded 2 phases ago), load A0(g+2)
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      swrite(RA1, g + 1, 0);
-      gload(RA0, g + 2, 0);
-    } else if (s1) stage(RA1, g + 1);
+    if (s1) stage(RA1, g + 1);
     barrier();
     lgkm0();
     mma(0, 0);
     barrier();
     // P2: quadrant (0,1)
     read_B(cur + RB1 * kRegion);
-    if constexpr (kReg) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      swrite(RB0, g + 1, 1);
-      gload(RB1, g + 2, 1);
-    } else if (s1) stage(RB0, g + 1);
+    if (s1) stage(RB0, g + 1);
     barrier();
     lgkm0();
     mma(0, 1);
     barrier();
     // P3: quadrant (1,1)
     read_A(cur + RA1 * kRegion);
-    if constexpr (kReg) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      swrite(RA0, g + 2, 0);
-      gload(RA1, g + 2, 0);
-    } else if (s2) stage(RA0, g + 2);
+    if (s2) stage(RA0, g + 2);
     barrier();
     lgkm0();
     mma(1, 1);
     barrier();
     // P4: quadrant (1,0)
     read_B(cur + RB0 * kRegion);
-    if constexpr (kReg) {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      swrite(RB1, g + 2, 1);
-      gload(RB0, g + 2, 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K-tile g+1 written before the barrier
-    } else if (s2) {
+    if (s2) {
       stage(RB1, g + 2);
-      if constexpr (!(DIAG & 8)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
-      if constexpr (!(DIAG & 8)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     barrier();
     lgkm0();
@@ -293,9 +220,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
     // ---- epilogue of tile j: lane holds D[n = nb + 16*ng + 4*(lane>>4) + r][m = mb + 16*mg] ----
     const int tile = first + j * stride;
     ++j;
-    if constexpr (DIAG & 32) {  // ablation: no epilogue (the accumulators stay live)
-      if (ep.ldo != -12345) continue;
-    }
     const int m0 = (tile / tilesN) * BM, n0 = (tile % tilesN) * BN;
     const int mb = m0 + wm * 128 + l16;
     const int nbase = n0 + wn * 64 + cq * 4;
@@ -342,20 +266,20 @@ int num_cus() {
   return n;
 }
 
-template <int EPI, int DIAG = 0>
+template <int EPI>
 hipError_t launch_one(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                       int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<EPI, DIAG>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus() ? tiles : num_cus();
-  VP_NOTE_KERNEL((gemm_bf16_tn_kernel<EPI, DIAG>));
-  hipLaunchKernelGGL((gemm_bf16_tn_kernel<EPI, DIAG>), dim3(grid), dim3(kGemmThreads), kGemmLds, s, A, lda,
+  VP_NOTE_KERNEL((gemm_bf16_tn_kernel<EPI>));
+  hipLaunchKernelGGL((gemm_bf16_tn_kernel<EPI>), dim3(grid), dim3(kGemmThreads), kGemmLds, s, A, lda,
                      W, ldw, M, N, K, ep);
   return hipGetLastError();
 }
@@ -370,27 +294,6 @@ const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw) {
   if (lda < K || ldw < K || (lda % 8) || (ldw % 8)) return "gemm: bad leading dimension";
   return nullptr;
 }
-
-#ifdef VP_DIAG
-hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
-                          int M, int N, int K, const EpiArgs& ep, hipStream_t s) {
-  switch (diag) {
-    case 0: return launch_one<EPI_BF16, 0>(A, lda, W, ldw, M, N, K, ep, s);
-    case 1: return launch_one<EPI_BF16, 1>(A, lda, W, ldw, M, N, K, ep, s);
-    case 2: return launch_one<EPI_BF16, 2>(A, lda, W, ldw, M, N, K, ep, s);
-    case 3: return launch_one<EPI_BF16, 3>(A, lda, W, ldw, M, N, K, ep, s);
-    case 4: return launch_one<EPI_BF16, 4>(A, lda, W, ldw, M, N, K, ep, s);
-    case 7: return launch_one<EPI_BF16, 7>(A, lda, W, ldw, M, N, K, ep, s);
-    case 8: return launch_one<EPI_BF16, 8>(A, lda, W, ldw, M, N, K, ep, s);
-    case 10: return launch_one<EPI_BF16, 10>(A, lda, W, ldw, M, N, K, ep, s);
-    case 16: return launch_one<EPI_BF16, 16>(A, lda, W, ldw, M, N, K, ep, s);
-    case 32: return launch_one<EPI_BF16, 32>(A, lda, W, ldw, M, N, K, ep, s);
-    case 33: return launch_one<EPI_BF16, 33>(A, lda, W, ldw, M, N, K, ep, s);
-    case 34: return launch_one<EPI_BF16, 34>(A, lda, W, ldw, M, N, K, ep, s);
-  }
-  return hipErrorInvalidValue;
-}
-#endif
 
 hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                      int N, int K, const EpiArgs& ep, hipStream_t s) {

@@ -446,33 +446,14 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
   return VP_OK;
 }
 
-#ifdef VP_DIAG
-// Not in the public header: ablation builds of the bf16 GEMM (tools/gemm_bench.py).
-int vp_dev_gemm_diag(int diag, const void* A, const void* W, int64_t M, int64_t N, int64_t K,
-                     void* out, const float* bias, void* stream) {
-  using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
-  EpiArgs ep;
-  ep.out = out; ep.ldo = N; ep.bias = bias;
-  VP_HIP(gemm_bf16_diag(diag, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
-                        static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-#endif
-
-// Not in the public header: one named bf16 GEMM kernel (4: gemm_bf16_w4, 8: gemm_bf16; the tools'
-// diag library adds 2: gemm_bf16_ov)
-// with any epilogue, for kernel A/B tests (tests/test_gpu_kernels.py) and tools/gemm_bench.py.
-// epi >= 1000 selects the 4-wave kernel's ablation builds.
+// Not in the public header: one named bf16 GEMM kernel (4: gemm_bf16_w4, 8: gemm_bf16) with any
+// epilogue, for kernel A/B tests (tests/test_gpu_kernels.py) and tools/gemm_bench.py.
 int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t M, int64_t N,
                        int64_t K, void* out, const float* bias, const void* resid, const float* pos,
                        int64_t pos_rows, const float* rowpad, void* stream) {
   using namespace vp;
-  if (which != 2) {
-    const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-    if (e) return fail(VP_EINVAL, e);
-  }
+  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
   ep.pos = pos; ep.pos_rows = (int)(pos_rows > 0 ? pos_rows : 1); ep.rowpad = rowpad;
@@ -481,15 +462,8 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
     VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
   else if (which == 8)
     VP_HIP(gemm_bf16(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
-#ifdef VP_DIAG
-  else if (which == 2) {
-    if (!gemm_bf16_ov_ok(epi >= 1000 ? 0 : epi, (int)M, (int)N, (int)K, K, K))
-      return fail(VP_EINVAL, "shape/epilogue not supported by gemm_bf16_ov");
-    VP_HIP(gemm_bf16_ov(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
-  }
-#endif
   else
-    return fail(VP_EINVAL, "which must be 4 or 8 (2: diag library)");
+    return fail(VP_EINVAL, "which must be 4 or 8");
   return VP_OK;
 }
 
@@ -501,10 +475,7 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
                    const float* rowpad, const float* ln_rs, const float* ln_c, float* st_part,
                    void* stream) {
   using namespace vp;
-  if ((epi < EPI_BF16_LN || epi > EPI_POS_BF16_ST) && epi != 3009 && epi != 3010 && epi != 3011 && epi != 3013 &&
-      epi != 10111)
-    return fail(VP_EINVAL, "epilogue must be 8..12 (diag: 3009 ffn1 with the rowpad multiply, 3010 scalar GELU, "
-                           "3011 ungrouped, 3013 XCD-pair order)");
+  if (epi < EPI_BF16_LN || epi > EPI_POS_BF16_ST) return fail(VP_EINVAL, "epilogue must be 8..12");
   const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
@@ -515,49 +486,6 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
                       static_cast<hipStream_t>(stream)));
   return VP_OK;
 }
-
-#ifdef VP_DIAG
-// diag library only: the 8-wave GEMM with the 4-wave pipeline (tools/diag/csrc/gemm_bf16_w8b.hip),
-// EPI_BF16 / EPI_GELU_BF16_LN, for tools/ab_tests.py and tools/gemm_bench.py w8b (diag 8: no epilogue)
-int vp_dev_gemm_w8b(int epi, int diag, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
-                    const float* bias, const float* rowpad, const float* ln_rs, const float* ln_c, void* stream) {
-  using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
-  EpiArgs ep;
-  ep.out = out; ep.ldo = N; ep.bias = bias; ep.rowpad = rowpad; ep.ln_rs = ln_rs; ep.ln_c = ln_c;
-  VP_HIP(gemm_bf16_w8b(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, diag,
-                       static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-
-// diag library only: the fused q|k|v projection + spatial attention kernel (an experiment that
-// measured no faster than the unfused pair; tools/qa_bench.py checks it bitwise
-// against vp_dev_gemm_ln(EPI_BF16_LN) + vp_op_attention)
-int vp_dev_qkv_attention(const void* x, const float* ln_rs, const void* wqkv, const float* bias,
-                         const float* lnc, void* out, int64_t frames, int64_t heads, float cap, void* stream) {
-  using namespace vp;
-  if (!qkv_attention_spatial_ok((int)frames, (int)heads, cap < -1000.f ? 50.f : cap))
-    return fail(VP_EINVAL, "qkv_attention: needs heads*64 == 768, cap > 0 and frames*256 rows in range");
-  if (cap < -1000.f) {  // ablation builds: cap = -1000 - diag (tools/qa_bench.py)
-    VP_HIP(qkv_attention_spatial_diag((int)(-1000.f - cap), (const bf16_t*)x, ln_rs, (const bf16_t*)wqkv, bias,
-                                      lnc, (bf16_t*)out, (int)frames, (int)heads, 50.f,
-                                      static_cast<hipStream_t>(stream)));
-    return VP_OK;
-  }
-  VP_HIP(qkv_attention_spatial_bf16((const bf16_t*)x, ln_rs, (const bf16_t*)wqkv, bias, lnc, (bf16_t*)out,
-                                    (int)frames, (int)heads, cap, static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-
-// ablation builds of the spatial attention kernel (tools/attn_bench.py)
-int vp_dev_attention_diag(int diag, const void* qkv, void* o, int64_t num_seq, int64_t heads, float cap,
-                          void* stream) {
-  VP_HIP(vp::attention_spatial_diag(diag, (const vp::bf16_t*)qkv, (vp::bf16_t*)o, (int)num_seq, (int)heads, cap,
-                                    static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-#endif
 
 // which = 0: ln_stats_finalize(src = st_part [D/128][M][2]); 1: ln_row_stats(src = bf16 [M][D])
 int vp_dev_ln_stats(int which, const void* src, int64_t M, int64_t D, float* ln_rs, void* stream) {

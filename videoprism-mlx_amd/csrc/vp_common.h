@@ -106,6 +106,46 @@ __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1
 
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// ---- LDS reads hipcc must not wait for with vmcnt (the attention kernels' K/V chunks land by
+// LDS-DMA while earlier chunks are read; a compiler-visible read there gets a vmcnt(0) in front
+// of it).  Each helper issues its reads AND their lgkmcnt(0) in ONE asm statement with
+// early-clobber outputs (cdna_hip_programming.md §5.7 item 1, form (i)): the destination
+// registers are defined only after the data has landed, so no compiler copy, spill or reuse can
+// touch them while a read is in flight.  tools/check_kernels.py rejects any asm load with a VGPR
+// destination that does not carry its wait in the same statement. ----
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// 8 transposed reads (ds_read_b64_tr_b16) at ad[s][dh] and ad[s][dh] + 1024 -> v[s][dh][0 / 1]
+__device__ __forceinline__ void lds_tr_read8(s16x4 (&v)[2][2][2], const uint32_t (&ad)[2][2]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8\n\t"
+      "ds_read_b64_tr_b16 %1, %8 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %2, %9\n\t"
+      "ds_read_b64_tr_b16 %3, %9 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %4, %10\n\t"
+      "ds_read_b64_tr_b16 %5, %10 offset:1024\n\t"
+      "ds_read_b64_tr_b16 %6, %11\n\t"
+      "ds_read_b64_tr_b16 %7, %11 offset:1024\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0][0][0]), "=&v"(v[0][0][1]), "=&v"(v[0][1][0]), "=&v"(v[0][1][1]), "=&v"(v[1][0][0]),
+        "=&v"(v[1][0][1]), "=&v"(v[1][1][0]), "=&v"(v[1][1][1])
+      : "v"(ad[0][0]), "v"(ad[0][1]), "v"(ad[1][0]), "v"(ad[1][1])
+      : "memory");
+}
+
+// 4 reads of 16 B (ds_read_b128) at ad[i] -> v[i]
+__device__ __forceinline__ void lds_read4_b128(bf16x8 (&v)[4], const uint32_t (&ad)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %5\n\t"
+      "ds_read_b128 %2, %6\n\t"
+      "ds_read_b128 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
+      : "memory");
+}
+
 // ReLU that keeps a NaN a NaN like jax.nn.relu (text tower ffn_layer1, encoders.py:743): IEEE-754-2019
 // maximum (gfx950 v_maximum3_f32), not maxNum
 __device__ __forceinline__ float relu_nan(float x) { return __builtin_elementwise_maximum(x, 0.0f); }

@@ -531,11 +531,10 @@ struct Fwd {
     const int epi_resid = xbf ? EPI_RESID_BF16 : EPI_RESID_F32;
     const int epi_resid_ffn = xbf ? EPI_RESID_FFN_BF16 : EPI_RESID_FFN;
     // temporal attention fused into the q|k|v projection (vp_kernels.h EPI_*_TATTN_LN): T = 16
-    // frames (one 16-row MFMA block per sequence), dh = 64, no key paddings, max-free cap
-    // (VP_NO_TATTN=1 in the environment keeps the unfused pair: A/B measurements only)
-    static const bool tattn_off = std::getenv("VP_NO_TATTN") != nullptr;
+    // frames (one 16-row MFMA block per sequence), dh = 64, no key paddings, max-free cap; the
+    // unfused pair stays for every other temporal case (frame paddings, T != 16, other caps)
     const bool tattn = fold && xbf && kind == ATT_VIDEO && S == 16 && !pad && fast_cap(cap) && D == NH * 64 &&
-                       !layers.empty() && layers[0].wqk && M % 256 == 0 && !tattn_off;
+                       !layers.empty() && layers[0].wqk && M % 256 == 0;
     for (size_t li = 0; li < layers.size(); ++li) {
       LayerW& lw = layers[li];
       const bool last = li + 1 == layers.size();
@@ -543,6 +542,8 @@ struct Fwd {
         // P (normalised bf16 probabilities, 512 B per (sequence, head)) goes to `big`; O to hb
         vp::EpiArgs ep;
         ep.ln_rs = ln_rs; ep.cap = cap; ep.heads = NH;
+        ep.cap_c1 = 2.0f * 1.4426950408889634f / cap;  // the same IEEE division the kernel did
+        ep.cap_c2 = cap * 1.4426950408889634f;
         ep.out = big; ep.bias = lw.bqk; ep.ln_c = lw.cqk;
         VP_HIP(rec(PC_GEMM_QKV_TATTN, 2.0 * dM * dD * 2 * dD + 4.0 * num_seq * (double)S * S * dD,
                    gbytes(dD, 2 * dD, 0, 0) + dM * NH * 32.0, [&] {

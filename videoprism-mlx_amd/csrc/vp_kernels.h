@@ -67,6 +67,9 @@ struct EpiArgs {
   float* st_part = nullptr;       // EPI_*_ST: [N/128][M][2] partial (sum, M2) of each row
   int64_t st_rows = 0;            // EPI_*_ST: M (partial stride)
   float cap = 0.0f;               // EPI_*_TATTN_LN: logit cap (0 < cap <= 50)
+  // EPI_QK_TATTN_LN: 2 log2(e) / cap and cap log2(e), the capped-exp constants (host-computed: a
+  // kernel argument lives in SGPRs, the in-kernel division's result in two VGPRs across the loop)
+  float cap_c1 = 0.0f, cap_c2 = 0.0f;
   int heads = 0;                  // EPI_*_TATTN_LN: heads of the whole projection (P indexing)
 };
 
@@ -79,24 +82,11 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 // staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
-// N-tile group size of the persistent tile order (gemm_bf16_w4.hip; shared by gemm_bf16_w8b)
+// N-tile group size of the persistent tile order (gemm_bf16_w4.hip; shared by the diag kernels)
 int w4_ngrp(int M, int N, int K, int grid);
-// diag library only: 8-wave form of the 4-wave kernel's pipeline (two 128x64 waves per SIMD,
-// tools/diag/csrc/gemm_bf16_w8b.hip): EPI_BF16 / EPI_GELU_BF16_LN; diag 8 = no epilogue
-hipError_t gemm_bf16_w8b(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
-                         int K, const EpiArgs& ep, int diag, hipStream_t s);
-// [diag library only] 4-wave, 256x128 tile, two accumulator sets: the epilogue of tile j runs under the MFMAs of
-// tile j+1 (gemm_bf16_ov.hip).  bf16-output epilogues, M % 256, N % 128, K % 64, K >= 704.
-bool gemm_bf16_ov_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw);
-hipError_t gemm_bf16_ov(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
-                        int N, int K, const EpiArgs& ep, hipStream_t s);
 // picks gemm_bf16_w4 or gemm_bf16 by epilogue and shape
 hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                           int N, int K, const EpiArgs& ep, hipStream_t s);
-
-// [diag library only] ablation builds of the bf16 GEMM (store epilogue) for tools/gemm_bench.py
-hipError_t gemm_bf16_diag(int diag, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
-                          int M, int N, int K, const EpiArgs& ep, hipStream_t s);
 
 // ---- fp32 GEMM for fprop_dtype=float32 (gemm_f32.hip) ----
 const char* gemm_f32_check(int M, int N, int K);
@@ -106,22 +96,8 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
 // ---- attention (attention.hip) ----
 // qkv: rows of [q(D) | k(D) | v(D)], row r = seq * S + s; q pre-scaled by dh^-0.5.
 // o: rows of D = heads*64.  key_pad: optional [num_seq * S] (1 = padded key).
-// diag library only (A/B experiment, measured no faster than the unfused pair):
-// q|k|v projection (LN1 folded, EPI_BF16_LN arithmetic) + spatial attention (S = 256, dh = 64,
-// D = 768, no key paddings) fused per (frame, head) (qkv_attention.hip); bitwise equal to
-// gemm_bf16_w4(EPI_BF16_LN) followed by attention_spatial_bf16.
-bool qkv_attention_spatial_ok(int frames, int heads, float cap);
-hipError_t qkv_attention_spatial_bf16(const bf16_t* x, const float* ln_rs, const bf16_t* wqkv, const float* bias,
-                                      const float* lnc, bf16_t* o, int frames, int heads, float cap,
-                                      hipStream_t s);
-hipError_t qkv_attention_spatial_diag(int diag, const bf16_t* x, const float* ln_rs, const bf16_t* wqkv,
-                                      const float* bias, const float* lnc, bf16_t* o, int frames, int heads,
-                                      float cap, hipStream_t s);
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, const float* key_pad, hipStream_t s);
-// [diag library only] ablation builds of the spatial kernel (tools/attn_bench.py)
-hipError_t attention_spatial_diag(int diag, const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
-                                  float cap, hipStream_t s);
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s);
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,

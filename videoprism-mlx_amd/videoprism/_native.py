@@ -144,10 +144,11 @@ _SIGNATURES = {
 _DIAG_SIGNATURES = {
     "vp_dev_gemm_w8b": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_void_p, c_void_p]),
-    "vp_dev_attention_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_attention_qh": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
-    "vp_dev_gemm_diag": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
-                                 c_void_p, c_void_p]),
+    "vp_dev_gemm_w4_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
+                                   c_void_p, c_void_p]),
+    "vp_dev_gemm_ov": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
     "vp_dev_qkv_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                      c_int64, c_int64, c_float, c_void_p]),
 }
@@ -282,6 +283,25 @@ def dev_gemm_w8b(a, w, bias, epilogue, out, rowpad=None, ln_rs=None, ln_c=None, 
     N = w.shape[0]
     call("vp_dev_gemm_w8b", epilogue, diag, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(rowpad),
          _ptr(ln_rs), _ptr(ln_c), _stream(stream))
+    return out
+
+
+def dev_gemm_w4_abl(a, w, bias, out, abl, s3=False, stream=None):
+    """Diag library only: an ablation build of the product 4-wave GEMM (EPI_BF16; abl 2 = no
+    ds_reads, 4 = no staging loads, 8 = no epilogue) -- timing only, results garbage."""
+    M, K = a.shape
+    N = w.shape[0]
+    call("vp_dev_gemm_w4_abl", abl, 1 if s3 else 0, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias),
+         _stream(stream))
+    return out
+
+
+def dev_gemm_ov(a, w, bias, epilogue, out, resid=None, stream=None):
+    """Diag library only: the overlapped-epilogue GEMM (tools/diag/csrc/gemm_bf16_ov.hip)."""
+    M, K = a.shape
+    N = w.shape[0]
+    call("vp_dev_gemm_ov", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
+         _stream(stream))
     return out
 
 
