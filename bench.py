@@ -103,6 +103,8 @@ def cpu_baseline(cfg, variables, runs: int = 3) -> dict:
                 times.append(time.perf_counter() - t0)
     mean, std = float(np.mean(times)), float(np.std(times))
     return {"value": round(1.0 / mean, 5), "unit": "clips/s", "cores": int(threads), "kind": "port",
+            "blas_threads": int(threads), "host_cpus_schedulable": len(os.sched_getaffinity(0)),
+            "host_cpus_total": os.cpu_count(),
             "sample": f"1 clip [1,16,288,288,3], full {cfg.get('_name', 'model')} forward, NumPy fp32 "
                       f"oracle (oracle/videoprism_oracle.py): 1 warm-up + {runs} timed runs, "
                       f"{mean:.2f} +- {std:.2f} s per clip (min {min(times):.2f}, max {max(times):.2f}) "
@@ -264,14 +266,30 @@ def main() -> None:
     if args.hang_rank >= 0 and int(os.environ.get("RANK", 0)) == args.hang_rank:
         time.sleep(3600)  # a rank that never joins (same tests)
 
-    import torch
-
-    from videoprism import _native, distributed, models, params
+    from videoprism import distributed
 
     # the process group is CPU-side (gloo) on GPU ranks too: it carries only the rendezvous, the
     # RCCL id broadcast, the barrier and the max-over-ranks; the library's vp_comm is each rank's
     # only RCCL communicator
     rank, local_rank, world = distributed.init("gloo")
+    owned = []  # the RCCL communicator, once created
+    try:
+        _run(args, rank, local_rank, world, owned)
+    finally:
+        # orderly teardown on every exit path: the RCCL communicator first (its destroy
+        # synchronises with the peers), then the process group
+        for c in owned:
+            c.close()
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
+    """The bench proper, between the process group's creation and its teardown (main)."""
+    import torch
+
+    from videoprism import _native, distributed, models, params
     if world != args.gpus:
         print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
@@ -289,19 +307,27 @@ def main() -> None:
         if lvt:
             cfg["vocabulary_size"] = 32000
     else:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device(f"cuda:{local_rank}")
+        if world > 1 and os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY") != "0":
+            # the host driver supports dmabuf IPC only: RCCL's peer setup needs the legacy mode off
+            print("bench: warning: HSA_ENABLE_IPC_MODE_LEGACY is not 0; RCCL may fail with "
+                  "'hipIpcGetMemHandle: invalid argument' (export HSA_ENABLE_IPC_MODE_LEGACY=0)",
+                  file=sys.stderr, flush=True)
+        local_dev = distributed.local_device(local_rank)
+        torch.cuda.set_device(local_dev)
+        dev = torch.device(f"cuda:{local_dev}")
         model = models.get_model(name, fprop_dtype=torch.bfloat16)
         if lvt:
             cfg["vocabulary_size"] = model.vocabulary_size
             variables = params.synthetic_params(cfg, seed=0, specs=params.clip_leaf_specs(cfg))
         else:
             variables = params.synthetic_params(cfg, seed=0)
-        eng = model.engine(variables, local_rank)
+        eng = model.engine(variables, local_dev)
         ops = GpuOps(eng, _native)
         gen = torch.Generator(device=dev).manual_seed(1000 + rank)
         video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev).to(torch.bfloat16)
-        comm = distributed.Communicator(local_rank) if gather else None
+        comm = distributed.Communicator(local_dev) if gather else None
+        if comm is not None:
+            owned.append(comm)
 
     last = {}
     if lvt:
@@ -444,12 +470,6 @@ def main() -> None:
             line.update({"data": "CPU stand-in forward (--standin): plumbing test, not a measurement",
                          "dtype": "f32", "standin_check": standin_check})
         print(json.dumps(line), flush=True)
-
-    if comm is not None:
-        comm.close()
-    import torch.distributed as dist
-    if dist.is_initialized():
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

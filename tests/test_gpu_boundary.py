@@ -113,6 +113,41 @@ def test_rccl_allgather_one_rank(cuda):
         dist.destroy_process_group()
 
 
+def test_allgather_side_stream_ordering(cuda):
+    """Communicator.all_gather_rows on an explicit side stream: the rows are produced on the current
+    stream by a long chain of kernels right before the call, and the result is consumed on the
+    current stream right after it, with no synchronisation by the caller.  The gather must see the
+    finished rows (the side stream waits for the current one) and the consumer the finished gather
+    (the current stream waits for the side one); repeated with fresh allocations so a reuse of
+    recorded memory would show.  (Uneven shards need world > 1: tests/test_distributed_cpu.py.)"""
+    import socket
+
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        with distributed.Communicator(0) as comm:
+            side = torch.cuda.Stream(device=cuda)
+            big = torch.randn(4096, 4096, device=cuda)
+            for it in range(4):
+                x = torch.zeros(64, 768, device=cuda)
+                for _ in range(8):  # keeps the current stream busy for a while
+                    big = (big @ big).clamp_(-1.0, 1.0)
+                x += float(it + 1)
+                x += big[:64, :768] * 0.0
+                y = comm.all_gather_rows(x, stream=side, counts=[64])
+                z = y * 2.0  # consumed on the current stream
+                del x
+                torch.cuda.synchronize()
+                assert torch.equal(z, torch.full_like(z, 2.0 * (it + 1))), it
+    finally:
+        dist.destroy_process_group()
+
+
 def test_bench_base_step_world1_gather_vs_fixture(cuda):
     """bench.py's real base step at world 1 -- Engine.forward -> op_pool_l2 -> the library's RCCL
     gather (Communicator.all_gather_rows over a one-rank communicator, bootstrapped through a gloo

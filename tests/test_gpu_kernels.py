@@ -438,3 +438,57 @@ def test_gemm_row_stats(cuda, epi):
     assert torch.allclose(rs_p.double(), ref, rtol=2e-5, atol=1e-5)
     assert torch.allclose(rs_r.double(), ref, rtol=2e-5, atol=1e-5)
 
+
+
+@pytest.mark.parametrize("heads", [12, 16])
+def test_temporal_attention_fused_kernels_vs_unfused(cuda, heads):
+    """The two fused temporal-attention launches (EPI_QK_TATTN_LN -> P, EPI_V_TATTN_LN -> O) on one
+    layer with many GEMM tiles (M = 8192 rows = 512 sequences of T = 16; Base and Large head counts)
+    against the unfused pair on the same inputs: the LN-folded q|k|v GEMM (EPI_BF16_LN) then the
+    temporal attention kernel.  q, k, v are the same bf16 values on both paths; the fused path
+    rounds the normalised probabilities to bf16 (the reference's probs.astype(fprop)), the unfused
+    kernel the unnormalised numerators, so per element |O_f - O_u| <= 2^-6 |O_u| + 2^-7 max|v| of the
+    (sequence, head) -- a few bf16 ulps -- with the mean far below.  Also against fp64 attention on
+    the unfused path's bf16 q|k|v."""
+    D = heads * 64
+    M, S = 8192, 16
+    nseq = M // S
+    g = torch.Generator(device="cpu").manual_seed(heads)
+    x = _bf(torch.randn(M, D, generator=g) * 2 + 0.3)
+    w = torch.randn(3 * D, D, generator=g) / D ** 0.5
+    w[:D] *= 0.125 * 4  # q rows carry the folded dh^-0.5 (with some extra spread of the logits)
+    wp = _bf(w)
+    b = (torch.randn(3 * D, generator=g) * 0.1).float()
+    c = wp.double().sum(1).float()
+    xc, wpc, bc, cc = x.to(cuda), wp.to(cuda), b.to(cuda), c.to(cuda)
+    rs = torch.empty(M, 2, device=cuda)
+    nat.dev_ln_stats(xc, M, D, rs, from_partials=False)
+    # unfused: q|k|v (bf16) then the temporal kernel
+    qkv = torch.empty(M, 3 * D, device=cuda, dtype=torch.bfloat16)
+    nat.dev_gemm_ln(xc, wpc, bc, nat.EPI_BF16_LN, qkv, ln_rs=rs, ln_c=cc)
+    o_u = nat.op_attention(qkv, nseq, S, heads, 50.0)
+    # fused: [q_h | k_h] rows per head, then the v rows
+    perm = torch.cat([torch.cat([torch.arange(h * 64, h * 64 + 64), D + torch.arange(h * 64, h * 64 + 64)])
+                      for h in range(heads)])
+    wqk, bqk, cqk = wpc[perm.to(cuda)].contiguous(), bc[perm.to(cuda)].contiguous(), cc[perm.to(cuda)].contiguous()
+    p = torch.empty(nseq * heads * 256, device=cuda, dtype=torch.bfloat16)
+    nat.dev_gemm_tattn(0, xc, wqk, bqk, rs, cqk, p, heads, 50.0)
+    o_f = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    nat.dev_gemm_tattn(1, xc, wpc[2 * D:].contiguous(), bc[2 * D:].contiguous(), rs, cc[2 * D:].contiguous(), o_f,
+                       heads, 50.0, p=p)
+    torch.cuda.synchronize()
+    q = qkv.double().cpu().reshape(nseq, S, 3, heads, 64)
+    qh, kh, vh = q[:, :, 0], q[:, :, 1], q[:, :, 2]                       # [nseq, S, heads, 64]
+    logits = torch.einsum("nqhd,nkhd->nhqk", qh, kh)
+    logits = 50.0 * torch.tanh(logits / 50.0)
+    ref = torch.einsum("nhqk,nkhd->nqhd", torch.softmax(logits, -1), vh).reshape(M, D)
+    vmax = vh.abs().amax(dim=(1, 3), keepdim=True).expand(nseq, S, heads, 64).reshape(M, D)
+    of, ou = o_f.double().cpu(), o_u.double().cpu()
+    d = (of - ou).abs()
+    bound = 2 ** -6 * ou.abs() + 2 ** -7 * vmax
+    print(f"heads {heads}: fused vs unfused max {float(d.max()):.3e} mean {float(d.mean()):.3e}; vs fp64 "
+          f"fused {float((of - ref).abs().max()):.3e} unfused {float((ou - ref).abs().max()):.3e}")
+    assert bool((d <= bound).all()), float((d - bound).max())
+    assert float(d.mean()) <= 2e-3 * float(ou.abs().mean()) + 1e-4
+    for o in (of, ou):
+        assert bool(((o - ref).abs() <= 2 ** -7 * ref.abs() + 2 ** -7 * vmax).all())

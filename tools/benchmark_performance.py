@@ -17,7 +17,6 @@ from __future__ import annotations
 import argparse
 import os
 import resource
-import statistics
 import sys
 import time
 
@@ -29,12 +28,13 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
 DEFAULT_MODEL_NAME = "videoprism_lvt_public_v1_base"
 
 
-def _format_stats(times: list[float]) -> str:
-    if not times:
-        return "(no samples)"
-    mean = statistics.mean(times)
-    std = statistics.pstdev(times) if len(times) > 1 else 0.0
-    return f"mean={mean:.4f}s  std={std:.4f}s  min={min(times):.4f}s  max={max(times):.4f}s"
+def _summary(durations: list[float]) -> str:
+    """One line over the timed runs: count, median and spread in milliseconds (empty -> note)."""
+    if len(durations) == 0:
+        return "no timed runs"
+    ms = np.asarray(durations, dtype=np.float64) * 1e3
+    lo, med, hi = np.percentile(ms, [0, 50, 100])
+    return f"n={ms.size} median {med:.1f} ms (range {lo:.1f}-{hi:.1f} ms, sd {ms.std():.1f} ms)"
 
 
 def _rss_gb() -> float:
@@ -101,7 +101,7 @@ def benchmark_hip(args):
     durations = [run_once() for _ in range(args.runs)]
     print("runs:", args.runs, " warmup:", args.warmup)
     print("timings:", [f"{t:.4f}" for t in durations])
-    print("stats:", _format_stats(durations))
+    print("timing:", _summary(durations))
     print(f"ru_maxrss: {_rss_gb():.3f} GB")
 
 
@@ -125,7 +125,7 @@ def benchmark_oracle(args):
     durations = [run_once() for _ in range(args.oracle_runs)]
     print("runs:", args.oracle_runs, " warmup:", args.oracle_warmup)
     print("timings:", [f"{t:.4f}" for t in durations])
-    print("stats:", _format_stats(durations))
+    print("timing:", _summary(durations))
     print(f"ru_maxrss: {_rss_gb():.3f} GB")
 
 

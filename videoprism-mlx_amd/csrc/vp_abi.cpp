@@ -487,6 +487,29 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
   return VP_OK;
 }
 
+// Not in the public header: the two launches of the fused temporal attention (EPI_QK_TATTN_LN,
+// EPI_V_TATTN_LN; vp_kernels.h) for kernel-level tests (tests/test_gpu_kernels.py).  which = 0: A = x
+// [M][K], W = the [q_h | k_h]-regrouped LN-folded rows [2K][K] -> P (512 B per (sequence, head));
+// which = 1: W = the v rows [K][K], p = P -> O [M][K].  K = heads * 64, M % 256 == 0.
+int vp_dev_gemm_tattn(int which, const void* A, const void* W, int64_t M, int64_t K, void* out, const float* bias,
+                      const float* ln_rs, const float* ln_c, const void* p, int64_t heads, float cap, void* stream) {
+  using namespace vp;
+  if (which < 0 || which > 1 || !A || !W || !out || !bias || !ln_rs || !ln_c || (which == 1 && !p))
+    return fail(VP_EINVAL, "bad argument");
+  if (K != heads * 64 || M % 256 || !vpi::fast_cap(cap)) return fail(VP_EINVAL, "needs K = heads*64, M % 256, 0 < cap <= 50");
+  const int64_t N = which == 0 ? 2 * K : K;
+  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  if (e) return fail(VP_EINVAL, e);
+  EpiArgs ep;
+  ep.out = out; ep.ldo = K; ep.bias = bias; ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.resid = p;
+  ep.cap = cap; ep.heads = (int)heads;
+  ep.cap_c1 = 2.0f * 1.4426950408889634f / cap;
+  ep.cap_c2 = cap * 1.4426950408889634f;
+  VP_HIP(gemm_bf16_w4(which == 0 ? EPI_QK_TATTN_LN : EPI_V_TATTN_LN, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M,
+                      (int)N, (int)K, ep, static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // which = 0: ln_stats_finalize(src = st_part [D/128][M][2]); 1: ln_row_stats(src = bf16 [M][D])
 int vp_dev_ln_stats(int which, const void* src, int64_t M, int64_t D, float* ln_rs, void* stream) {
   using namespace vp;

@@ -139,6 +139,8 @@ _SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "vp_dev_gemm_tattn": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
@@ -310,6 +312,15 @@ def dev_qkv_attention(x, ln_rs, wqkv, bias, lnc, out, frames, heads, cap, stream
     out [frames*256, D] bf16; all tensors contiguous on the device."""
     call("vp_dev_qkv_attention", _ptr(x), _ptr(ln_rs), _ptr(wqkv), _ptr(bias), _ptr(lnc), _ptr(out),
          frames, heads, float(cap), _stream(stream))
+    return out
+
+
+def dev_gemm_tattn(which, a, w, bias, ln_rs, ln_c, out, heads, cap, p=None, stream=None):
+    """The fused temporal attention's launches: which 0 (w = [q_h | k_h] rows) -> P in `out`,
+    which 1 (w = v rows, p = P) -> O [M, D] in `out`; all tensors contiguous on the device."""
+    M, K = a.shape
+    call("vp_dev_gemm_tattn", which, _ptr(a), _ptr(w), M, K, _ptr(out), _ptr(bias), _ptr(ln_rs), _ptr(ln_c),
+         _ptr(p), heads, float(cap), _stream(stream))
     return out
 
 

@@ -25,6 +25,19 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
+def local_device(local_rank: int) -> int:
+    """The HIP device index of this rank: LOCAL_RANK when the process sees every GPU of the node
+    (torch.distributed.run's default), 0 when a launcher narrowed it to one GPU
+    (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES per rank); anything else is a launch error."""
+    import torch
+    n = torch.cuda.device_count()
+    if local_rank < n:
+        return local_rank
+    if n == 1:
+        return 0
+    raise RuntimeError(f"LOCAL_RANK {local_rank} but only {n} visible HIP devices")
+
+
 def init(backend: str = "gloo", timeout_s: float = 600.0):
     """Join the launcher's process group (a CPU `gloo` group by default: GPU data moves only
     through the library's RCCL communicator).  A rank that never arrives fails the others after
@@ -115,18 +128,34 @@ class Communicator:
         tail = tuple(local.shape[1:])
         if bmax == 0:
             return torch.empty((0,) + tail, dtype=local.dtype, device=local.device)
-        send = local
-        if b != bmax:
-            send = torch.zeros((bmax,) + tail, dtype=local.dtype, device=local.device)
-            send[:b].copy_(local)
-        full = torch.empty((self.world * bmax,) + tail, dtype=local.dtype, device=local.device)
-        s = stream if stream is not None else torch.cuda.current_stream(local.device)
-        _native.call("vp_allgather", self._h, ctypes.c_void_p(send.data_ptr()),
-                     ctypes.c_void_p(full.data_ptr()), send.numel(), _native._prec(local),
-                     ctypes.c_void_p(s.cuda_stream))
-        if all(c == bmax for c in counts):
-            return full
-        return torch.cat([full[r * bmax:r * bmax + c] for r, c in enumerate(counts)])
+        # Stream order: `local` was produced on the caller's current stream; the padding copy, the
+        # gather and the unpadding all run on `s`, which first waits for the current stream; the
+        # current stream then waits for `s`, so the caller can use the result right away.  Tensors
+        # allocated on one stream and used on the other are recorded on it, so the caching
+        # allocator does not hand their memory out while the other stream may still use it.
+        cur = torch.cuda.current_stream(local.device)
+        s = stream if stream is not None else cur
+        side = s != cur
+        if side:
+            s.wait_stream(cur)
+            local.record_stream(s)
+        with torch.cuda.stream(s):
+            send = local
+            if b != bmax:
+                send = torch.zeros((bmax,) + tail, dtype=local.dtype, device=local.device)
+                send[:b].copy_(local)
+            full = torch.empty((self.world * bmax,) + tail, dtype=local.dtype, device=local.device)
+            _native.call("vp_allgather", self._h, ctypes.c_void_p(send.data_ptr()),
+                         ctypes.c_void_p(full.data_ptr()), send.numel(), _native._prec(local),
+                         ctypes.c_void_p(s.cuda_stream))
+            if all(c == bmax for c in counts):
+                out = full
+            else:
+                out = torch.cat([full[r * bmax:r * bmax + c] for r, c in enumerate(counts)])
+        if side:
+            cur.wait_stream(s)
+            out.record_stream(cur)
+        return out
 
     def close(self) -> None:
         from . import _native
