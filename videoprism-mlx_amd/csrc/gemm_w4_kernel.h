@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         bl[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64);
         bh[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64 + 4);
       }
-      if constexpr (EpiTraits<EPI>::kLnVals && !EpiTraits<EPI>::kQkAttn) {
+      if constexpr (EpiTraits<EPI>::kLn) {  // (the fused temporal epilogues load theirs in the epilogue)
 #pragma unroll
         for (int nh = 0; nh < 2; ++nh) {
           cl[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64);
@@ -337,15 +337,20 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       // 16-row block mt of this wave's 128 rows is one (b n) sequence of T = 16 frames; the
       // wave's 128 columns are [q_h | k_h] of one head (QK launch) or v of two heads (V launch).
       // q, k, v are LN-folded and rounded to bf16 as the reference's bf16 projections are. ----
-      const int r16 = lane & 15, g4 = lane >> 4;
+      // lane-derived addresses of these epilogues are computed here, per tile, from an opaque copy
+      // of the lane id: hoisted out of the tile loop (the compiler's choice) they would all stay
+      // live through the K-loop next to the fragment registers and spill
+      int lid = lane;
+      asm volatile("" : "+v"(lid));
+      const int r16 = lid & 15, g4 = lid >> 4;
+      // The accumulators stay in AGPRs through the K-loop: both epilogues read them with VALU where
+      // they stand, and without this the allocator gives some of them VGPR homes and the K-loop's
+      // fragment registers no longer fit (the QK launch spilled 5 VGPRs to scratch)
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+a"(acc[nt][mt]));
       if constexpr (Tr::kQkAttn) {
-        // The accumulators stay in AGPRs through the K-loop: without this the allocator gives some
-        // of them VGPR homes (the epilogue reads them with VALU) and the K-loop's fragment registers
-        // no longer fit (5 VGPRs spilled to scratch)
-#pragma unroll
-        for (int nt = 0; nt < 8; ++nt)
-#pragma unroll
-          for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+a"(acc[nt][mt]));
         // logits^T = K Q^T (16x16x32 on the accumulator-layout operands, d in two halves), capped
         // softmax over the 16 keys in fp32, the normalised probabilities rounded to bf16 (the
         // reference's probs.astype(fprop)) and stored as this lane's P^T fragment: keys
@@ -361,7 +366,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         // constants are re-read per group from L1).
         const float c1 = ep.cap_c1, c2 = ep.cap_c2;
         const int head = n0 >> 7;
-        const uint32_t lane_off = (uint32_t)lane * 8u;  // this lane's 8 B of a 512-B P block
+        const uint32_t lane_off = (uint32_t)lid * 8u;  // this lane's 8 B of a 512-B P block
 #pragma unroll
         for (int mh = 0; mh < 2; ++mh) {
           float4 cc[4], bb[4];
@@ -430,57 +435,69 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         // O^T = V^T . P^T per (sequence mt, head nh) on 16x16x16 MFMAs: A = V^T by transposed
         // reads of the bf16 V block, B = this lane's P^T fragment; the result lands in the
         // accumulator layout (lane: query r16, d = 16 dt + 4 g4 + r) and replaces v there, so the
-        // store path below writes O with whole-line stores.  The V values take the fp32 scratch
-        // round trip of the store path (row segments, the LN constants of the put layout): folding
-        // them where the accumulators stand measured slower here (register spills, 209 vs 168 us).
-        char* sb0 = scr;
-        char* sb1 = scr + kScrBuf;
+        // store path below writes O with whole-line stores.  One LDS pass: v is LN-folded where the
+        // accumulators stand (lane: row r16, columns 16 q + 4 g4 .. +3 of block q), rounded to bf16
+        // and written row-major with one ds_write_b64 per block into a 2 KiB V block whose 8-byte
+        // units are swizzled by row (unit ^ (((row >> 1) & 3) << 2): conflict-free for these writes
+        // and for the transposed reads, which read 8 B of one row per lane and so see the swizzle
+        // only in their addresses).  (The first form took v through the fp32 scratch and back:
+        // 168 us per launch at the bench shape.)
         const bf16_t* pin = static_cast<const bf16_t*>(ep.resid);
         const int trq = r16 >> 2, trp = r16 & 3;
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt) {
-          // both heads of sequence mt: V blocks at sb1 and sb1 + 2 KiB, one LDS wait per sequence
+        auto vunit = [](int row, int u) { return row * 128 + ((u ^ (((row >> 1) & 3) << 2)) << 3); };
+        // the LN-fold constants of the wave's 128 columns go to LDS once (c at +4 KiB, b' at +4.5 KiB
+        // of the wave's scratch) and are read where needed: held in registers for both heads they
+        // spilled the accumulator-layout fold
+        char* lc = scr + 4096;
+        {
+          const float* src = (lid < 32 ? ep.ln_c : ep.bias) + n0 + 4 * (lid & 31);
+          *reinterpret_cast<float4*>(lc + (lid < 32 ? 0 : 512) + 16 * (lid & 31)) =
+              *reinterpret_cast<const float4*>(src);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the constants are in LDS
+        __builtin_amdgcn_wave_barrier();
+        // P^T fragment of (sequence mt, head nh) and (rstd, -mean*rstd) of row mt*16 + r16, one
+        // (sequence, head) ahead of their use
+        auto ld_p = [&](int mt, int nh) {
           const int64_t sq = (int64_t)(m0 + mt * 16) >> 4;
-          bf16x4 pb[2];
+          return *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + nh * 64) >> 6)) * 256 + lid * 4);
+        };
+        auto ld_rs = [&](int mt) { return *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + mt * 16 + r16)); };
+        bf16x4 pb_n = ld_p(0, 0);
+        float2 rs_n = ld_rs(0);
 #pragma unroll
-          for (int nh = 0; nh < 2; ++nh)
-            pb[nh] = *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + nh * 64) >> 6)) * 256 + lane * 4);
+        for (int nh = 0; nh < 2; ++nh) {
 #pragma unroll
-          for (int nh = 0; nh < 2; ++nh) {
-            {  // accumulator block -> fp32 scratch (put layout)
-              char* sb = sb0 + frow * 256;
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<f32x4*>(sb + (((q * 4 + (lane >> 4)) ^ (frow & 7)) << 4)) = acc[nh * 4 + q][mt];
+          for (int mt = 0; mt < 8; ++mt) {
+            char* vb = scr + (mt & 1) * 2048;  // double-buffered V block (16 rows x 64 bf16)
+            const bf16x4 pb = pb_n;
+            const f32x2_t r = f32x2_t(rs_n.x), m = f32x2_t(rs_n.y);
+            if (mt < 7 || nh == 0) {
+              pb_n = ld_p((mt + 1) & 7, nh + (mt == 7));
+              rs_n = ld_rs((mt + 1) & 7);
             }
 #pragma unroll
-            for (int pass = 0; pass < 2; ++pass) {  // row segments -> LN fold -> bf16 V rows
-              const int rl = pass * 8 + er;
-              const char* sb = sb0 + rl * 256;
-              const float4 lo = *reinterpret_cast<const float4*>(sb + (((2 * es) ^ (rl & 7)) << 4));
-              const float4 hi = *reinterpret_cast<const float4*>(sb + (((2 * es + 1) ^ (rl & 7)) << 4));
-              const f32x2_t r = f32x2_t(rs[mt][pass].x), m = f32x2_t(rs[mt][pass].y);
-              auto fold2 = [&](float x0, float x1, float c0, float c1, float b0, float b1) {
-                const f32x2_t o = __builtin_elementwise_fma(
-                    r, f32x2_t{x0, x1}, __builtin_elementwise_fma(m, f32x2_t{c0, c1}, f32x2_t{b0, b1}));
-                return pack_bf16x2(o.x, o.y);
-              };
-              *reinterpret_cast<epi_u32x4*>(sb1 + nh * 2048 + rl * 128 + es * 16) =
-                  epi_u32x4{fold2(lo.x, lo.y, cl[nh].x, cl[nh].y, bl[nh].x, bl[nh].y),
-                            fold2(lo.z, lo.w, cl[nh].z, cl[nh].w, bl[nh].z, bl[nh].w),
-                            fold2(hi.x, hi.y, ch[nh].x, ch[nh].y, bh[nh].x, bh[nh].y),
-                            fold2(hi.z, hi.w, ch[nh].z, ch[nh].w, bh[nh].z, bh[nh].w)};
+            for (int q = 0; q < 4; ++q) {
+              const int cofs = 4 * (nh * 64 + 16 * q + 4 * g4);
+              const float4 c = *reinterpret_cast<const float4*>(lc + cofs);
+              const float4 b = *reinterpret_cast<const float4*>(lc + 512 + cofs);
+              const f32x4& a = acc[nh * 4 + q][mt];
+              const f32x2_t lo = __builtin_elementwise_fma(
+                  r, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(m, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
+              const f32x2_t hi = __builtin_elementwise_fma(
+                  r, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(m, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
+              *reinterpret_cast<uint2*>(vb + vunit(r16, 4 * q + g4)) =
+                  make_uint2(pack_bf16x2(lo.x, lo.y), pack_bf16x2(hi.x, hi.y));
             }
-          }
-          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int nh = 0; nh < 2; ++nh)
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
-              const bf16x4 vf = w4_tr_read(sb1 + nh * 2048 + (4 * g4 + trq) * 128 + (16 * dt + 4 * trp) * 2);
-              acc[nh * 4 + dt][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pb[nh], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+              const bf16x4 vf = w4_tr_read(vb + vunit(4 * g4 + trq, 4 * dt + trp));
+              acc[nh * 4 + dt][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             }
+            __builtin_amdgcn_sched_barrier(0);  // one sequence's accumulator reads at a time
+          }
         }
       }
     }
