@@ -492,3 +492,36 @@ def test_temporal_attention_fused_kernels_vs_unfused(cuda, heads):
     assert float(d.mean()) <= 2e-3 * float(ou.abs().mean()) + 1e-4
     for o in (of, ou):
         assert bool(((o - ref).abs() <= 2 ** -7 * ref.abs() + 2 ** -7 * vmax).all())
+
+
+@pytest.mark.parametrize("frames", [3, 9])
+def test_patch_embed_fused_from_frames(cuda, frames):
+    """The fused patch embedding (gemm_bf16_w4_video: the GEMM stages its A tiles straight from the
+    bf16 frames, one K-tile per patch row, no patch tensor) against the two-kernel path
+    (patchify -> [M, 1024] patches -> GEMM) and against fp64 on the same bf16 frames: the sums differ
+    only in their fp32 order, so |fused - two-kernel| <= 2^-8 |ref| + 1e-5, and the fused result is
+    within one bf16 rounding of fp64.  Frames with large values in every patch's neighbours check
+    that the 128-B source windows' overlap into the next patch meets zero weights only."""
+    P, D = 18, 768
+    g = torch.Generator(device="cpu").manual_seed(frames)
+    v = _bf(torch.rand(frames, 16 * P, 16 * P, 3, generator=g) * 4 - 1)
+    k = torch.randn(P * P * 3, D, generator=g) / (P * P * 3) ** 0.5
+    kb = _bf(k)
+    b = torch.randn(D, generator=g) * 0.1
+    pos = torch.randn(256, D, generator=g) * 0.1
+    wv = torch.zeros(D, 64 * P)
+    for py in range(P):
+        wv[:, 64 * py:64 * py + 3 * P] = kb[py * 3 * P:(py + 1) * 3 * P].T
+    wk = torch.zeros(D, 1024)
+    wk[:, :P * P * 3] = kb.T
+    vd = v.to(cuda)
+    fused = torch.empty(frames * 256, D, device=cuda, dtype=torch.bfloat16)
+    nat.dev_patch_embed(vd, P, _bf(wv).to(cuda), b.to(cuda), pos.to(cuda), fused)
+    patches = nat.op_patchify(vd, P, 1024, torch.bfloat16)
+    two = nat.op_gemm(patches, _bf(wk).to(cuda), b.to(cuda), nat.EPI_POS_BF16, pos=pos.to(cuda))
+    torch.cuda.synchronize()
+    pt = orc.image_to_patch(v.double().numpy(), P).reshape(-1, P * P * 3)
+    ref = pt @ kb.double().numpy() + b.double().numpy() + np.tile(pos.double().numpy(), (frames, 1))
+    f, t = fused.double().cpu().numpy(), two.double().cpu().numpy()
+    assert np.all(np.abs(f - t) <= 2 ** -8 * np.abs(ref) + 1e-5), np.abs(f - t).max()
+    assert np.all(np.abs(f - ref) <= 2 ** -8 * np.abs(ref) + 1e-5), np.abs(f - ref).max()

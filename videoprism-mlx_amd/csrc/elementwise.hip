@@ -298,6 +298,29 @@ __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restr
   }
 }
 
+// f32 / uint8 frames -> bf16 frames in place of layout (the fused patch embedding reads bf16
+// frames): the same conversion the patchify kernels apply per value (to_f, then one RNE rounding),
+// so a forward over converted frames sees bitwise the values a bf16 caller would pass
+template <typename TI>
+__global__ __launch_bounds__(256) void video_bf16_kernel(const TI* __restrict__ x, bf16_t* __restrict__ y,
+                                                         int64_t n) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[4];
+    if constexpr (sizeof(TI) == 1) {
+      const uchar4 u = reinterpret_cast<const uchar4*>(x)[i];
+      v[0] = to_f<TI>(u.x); v[1] = to_f<TI>(u.y); v[2] = to_f<TI>(u.z); v[3] = to_f<TI>(u.w);
+    } else {
+      const float4 f = reinterpret_cast<const float4*>(x)[i];
+      v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    }
+    reinterpret_cast<uint2*>(y)[i] = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                                (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(to_f<TI>(x[i]));
+}
+
 __global__ __launch_bounds__(256) void expand_paddings_kernel(const float* __restrict__ fp, int B,
                                                               int T, int Nsp,
                                                               float* __restrict__ pad_btn,
@@ -431,6 +454,20 @@ hipError_t ln_stats_finalize(const float* st_part, int P, int64_t M, float* ln_r
 
 hipError_t ln_row_stats(const bf16_t* x, int64_t M, int D, float* ln_rs, hipStream_t s) {
   hipLaunchKernelGGL(ln_row_stats_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, M, D, ln_rs);
+  return hipGetLastError();
+}
+
+hipError_t video_to_bf16(const void* video, int in_dtype, bf16_t* out, int64_t n, hipStream_t s) {
+  const dim3 g(grid_for((n + 3) / 4, 256));
+  if (in_dtype == 2) {
+    VP_NOTE_KERNEL(video_bf16_kernel<uint8_t>);
+    hipLaunchKernelGGL(video_bf16_kernel<uint8_t>, g, dim3(256), 0, s, (const uint8_t*)video, out, n);
+  } else if (in_dtype == 0) {
+    VP_NOTE_KERNEL(video_bf16_kernel<float>);
+    hipLaunchKernelGGL(video_bf16_kernel<float>, g, dim3(256), 0, s, (const float*)video, out, n);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -75,11 +75,18 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // 7.78 -> 7.48 ms/step in the forward.  (Three A stages with all 16 pieces in h1 measured 468 vs
 // 475 us isolated and nothing in the forward; the lead time alone is not it -- spreading the
 // pieces over both phases is.)
+// AVID: A is the video itself (patch embedding without a patch tensor): bf16 frames
+// [frames][16P][16P][3] of a 16x16 patch grid, so a 256-row tile is one frame and a piece's 8 rows
+// are 8 horizontally adjacent patches; K-tile kt is patch row kt (P <= 21: its 3P channels-last
+// values are contiguous and fill the first 6P bytes of the 128-B K-tile row), i.e. K = 64 P with
+// W zero outside columns 64 kt + [0, 3P).  The 128-B source window of a row runs 128 - 6P bytes
+// into the next patch (or the next pixel row); those values meet zero W columns.  lda = the
+// pixel-row length in elements (16 P * 3); the buffer descriptor spans the M / 256 frames.
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
 // accumulators stay live).
-template <int EPI, bool NOPAD, bool S3, int ABL = 0>
+template <int EPI, bool NOPAD, bool S3, int ABL = 0, bool AVID = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
     int N, int K, int ngrp, EpiArgs ep) {
@@ -130,13 +137,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // Lane: row (lane>>3) of the piece, LDS chunk (lane&7) <- source chunk (lane&7)^swz(row);
   // swz(row) of piece i depends only on i & 1.
   const uint32_t a_rb = (uint32_t)(lda * 2), w_rb = (uint32_t)(ldw * 2);
-  const uint64_t a_bytes = (uint64_t)M * a_rb, w_bytes = (uint64_t)N * w_rb;
+  // AVID: a_rb = one pixel row of a frame; P = nk pixel rows per patch, 16 P rows per frame
+  const uint32_t prow_b = AVID ? (uint32_t)(6 * (K / BK)) : 0;    // bytes of one patch's pixel row
+  const uint32_t frame_b = AVID ? (uint32_t)(16 * (K / BK)) * a_rb : 0;
+  const uint64_t a_bytes = AVID ? (uint64_t)(M / BM) * frame_b : (uint64_t)M * a_rb;
+  const uint64_t w_bytes = (uint64_t)N * w_rb;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)(uint32_t)a_bytes, 0x00020000);
   const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, (int)(uint32_t)w_bytes, 0x00020000);
   const int prow = lane >> 3;
   const uint32_t cE = (uint32_t)((lane & 7) ^ swz(prow)) * 16;       // even pieces
   const uint32_t cO = (uint32_t)((lane & 7) ^ swz(prow + 8)) * 16;   // odd pieces
-  const uint32_t vA[2] = {prow * a_rb + cE, prow * a_rb + cO};
+  const uint32_t vA[2] = {prow * (AVID ? prow_b : a_rb) + cE, prow * (AVID ? prow_b : a_rb) + cO};
   const uint32_t vW[2] = {prow * w_rb + cE, prow * w_rb + cO};
   typedef __attribute__((address_space(3))) void lds_void;
   // load stream: K-tile ld_g -> (tile ld_tm/ld_tn, K-tile ld_kt); the tail re-loads the last
@@ -161,7 +172,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const int i = p & 7;
     char* dst = (p >= 8 ? w_buf(buf) : a_buf(buf)) + (w * 8 + i) * 1024;
     if (p < 8) {
-      const uint32_t so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
+      uint32_t so;
+      if constexpr (AVID) {  // piece w*8+i: patch-grid row (w*8+i) >> 1, patches 8 ((w*8+i) & 1) + 0..7
+        const int pc = w * 8 + i;
+        so = (uint32_t)ld_tm * frame_b + (uint32_t)((pc >> 1) * (K / BK) + ld_kt) * a_rb + (uint32_t)(pc & 1) * 8 * prow_b;
+      } else {
+        so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
+      }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
     } else {
       const uint32_t so = (uint32_t)(ld_tn * BN + (w * 8 + i) * 8) * w_rb + ld_kt * (BK * 2);
@@ -618,12 +635,12 @@ int num_cus_w4() {
   return n;
 }
 
-template <int EPI, bool NOPAD, bool S3, int ABL = 0>
+template <int EPI, bool NOPAD, bool S3, int ABL = 0, bool AVID = false>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL, AVID>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -631,8 +648,8 @@ hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw,
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
   const int ngrp = w4_ngrp(M, N, K, grid);
-  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL>));
-  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda,
+  VP_NOTE_KERNEL((gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL, AVID>));
+  hipLaunchKernelGGL((gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL, AVID>), dim3(grid), dim3(kThreads), kLdsTotal, s, A, lda,
                      W, ldw, M, N, K, ngrp, ep);
   return hipGetLastError();
 }

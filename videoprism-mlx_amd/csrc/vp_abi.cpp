@@ -116,6 +116,13 @@ int vp_finalize(vp_handle* h) {
     for (int64_t i = 0; i < kreal; ++i)
       for (int64_t n = 0; n < D; ++n) t[(size_t)n * h->kpad + i] = k[(size_t)i * D + n];
     if ((rc = upload_mat(h, t, &h->wpatch))) return rc;
+    if (is_bf16(h) && 3 * P <= 64) {  // one 64-column K-tile per patch row (gemm_bf16_w4_video)
+      std::vector<float> tv((size_t)D * 64 * P, 0.0f);
+      for (int64_t py = 0; py < P; ++py)
+        for (int64_t j = 0; j < 3 * P; ++j)
+          for (int64_t n = 0; n < D; ++n) tv[(size_t)n * 64 * P + py * 64 + j] = k[(size_t)(py * 3 * P + j) * D + n];
+      if ((rc = upload_mat(h, tv, &h->wpatch_v))) return rc;
+    }
     if ((rc = upload_f32(h, param_data(h, px + "patch_projection/linear/bias"), &h->bpatch))) return rc;
   }
   if ((rc = upload_f32(h, param_data(h, px + "spatial_pos_emb/emb_var"), &h->spatial_pos))) return rc;
@@ -278,14 +285,32 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
   // 1. tokenisation + patch projection + spatial pos-emb (encoders.py:436-514)
   const double kreal = (double)P_ * P_ * 3;
   const double in_es = in_dtype == VP_U8 ? 1 : in_dtype == VP_BF16 ? 2 : 4;
-  if (Mp > M) VP_HIP(hipMemsetAsync(static_cast<char*>(big) + (size_t)M * h->kpad * es, 0,
-                                    (size_t)(Mp - M) * h->kpad * es, s));
-  VP_HIP(f.rec(PC_PATCHIFY, 0.0, dM * kreal * in_es + dM * h->kpad * dE, [&] {
-    return patchify(video, in_dtype, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
   const bool fold = bf && c.num_spatial_layers > 0;  // LN1 of spatial layer 0 folded
-  VP_HIP(f.rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, dE, 0), [&] {
-    return f.gemm(fold ? EPI_POS_BF16_ST : epi_pos, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr,
-                  sp_pos, Nsp, nullptr); }));
+  // bf16 on a 16x16 patch grid: the patch embedding reads the frames themselves (no patch
+  // tensor); f32 / uint8 frames are converted to bf16 frames first (the patchify kernels' per-value
+  // conversion, so every input dtype gives bitwise the bf16 caller's result)
+  if (h->wpatch_v && H / P_ == 16 && W / P_ == 16 && Mp == M) {
+    const bf16_t* frames = static_cast<const bf16_t*>(video);
+    if (in_dtype != VP_BF16) {
+      VP_HIP(f.rec(PC_PATCHIFY, 0.0, dM * kreal * (in_es + dE), [&] {
+        return video_to_bf16(video, in_dtype, static_cast<bf16_t*>(big), (int64_t)B * T * H * W * 3, s); }));
+      frames = static_cast<const bf16_t*>(big);
+    }
+    EpiArgs ep;
+    ep.out = x; ep.ldo = D; ep.bias = h->bpatch; ep.pos = sp_pos; ep.pos_rows = Nsp;
+    ep.st_part = f.st_part; ep.st_rows = Mp;
+    VP_HIP(f.rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, dE, 0), [&] {
+      return gemm_bf16_w4_video(fold ? EPI_POS_BF16_ST : EPI_POS_BF16, frames, P_, (const bf16_t*)h->wpatch_v, Mp, D,
+                                ep, s); }));
+  } else {
+    if (Mp > M) VP_HIP(hipMemsetAsync(static_cast<char*>(big) + (size_t)M * h->kpad * es, 0,
+                                      (size_t)(Mp - M) * h->kpad * es, s));
+    VP_HIP(f.rec(PC_PATCHIFY, 0.0, dM * kreal * in_es + dM * h->kpad * dE, [&] {
+      return patchify(video, in_dtype, big, bf, (int)(B * T), (int)H, (int)W, 3, P_, h->kpad, s); }));
+    VP_HIP(f.rec(PC_GEMM_PATCH, 2.0 * dM * kreal * dD, gbytes(kreal, dD, dE, 0), [&] {
+      return f.gemm(fold ? EPI_POS_BF16_ST : epi_pos, big, h->kpad, h->wpatch, D, x, D, h->bpatch, nullptr,
+                    sp_pos, Nsp, nullptr); }));
+  }
   const double ln_bytes = dM * dD * dE + dM * dD * dE;
   if (fold) VP_HIP(f.finalize());
   auto run_stack = [&](std::vector<LayerW>& layers, void* xs, int num_seq, int S, const float* pad) -> int {
@@ -507,6 +532,21 @@ int vp_dev_gemm_tattn(int which, const void* A, const void* W, int64_t M, int64_
   ep.cap_c2 = cap * 1.4426950408889634f;
   VP_HIP(gemm_bf16_w4(which == 0 ? EPI_QK_TATTN_LN : EPI_V_TATTN_LN, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M,
                       (int)N, (int)K, ep, static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
+// Not in the public header: the fused patch embedding (gemm_bf16_w4_video, EPI_POS_BF16) for kernel
+// tests: bf16 frames [frames][16P][16P][3], wv [N][64 P] (patch row py at columns 64 py + [0, 3P)),
+// pos [256][N] fp32 -> out [frames*256][N] bf16.
+int vp_dev_patch_embed(const void* video, int64_t frames, int64_t P, const void* wv, int64_t N, const float* bias,
+                       const float* pos, void* out, void* stream) {
+  using namespace vp;
+  if (!video || !wv || !bias || !pos || !out || frames < 1 || P < 1 || 3 * P > 64 || N % 256)
+    return fail(VP_EINVAL, "bad argument");
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias; ep.pos = pos; ep.pos_rows = 256;
+  VP_HIP(gemm_bf16_w4_video(EPI_POS_BF16, (const bf16_t*)video, (int)P, (const bf16_t*)wv, (int)(frames * 256), (int)N,
+                            ep, static_cast<hipStream_t>(stream)));
   return VP_OK;
 }
 

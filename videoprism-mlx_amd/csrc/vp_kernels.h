@@ -82,6 +82,11 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 // staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
+// patch embedding straight from bf16 frames (no patch tensor): video [M/256 frames]
+// [16P][16P][3] (a 16x16 patch grid, so one 256-row tile is one frame), W [N][64 P] with patch row
+// py's 3P values at columns 64 py + [0, 3P) and zeros elsewhere; epi EPI_POS_BF16(_ST)
+hipError_t gemm_bf16_w4_video(int epi, const bf16_t* video, int P, const bf16_t* W, int M, int N, const EpiArgs& ep,
+                              hipStream_t s);
 // N-tile group size of the persistent tile order (gemm_bf16_w4.hip; shared by the diag kernels)
 int w4_ngrp(int M, int N, int K, int grid);
 // picks gemm_bf16_w4 or gemm_bf16 by epilogue and shape
@@ -116,6 +121,9 @@ hipError_t patchify(const void* video, int in_dtype, void* patches, int out_is_b
 hipError_t layernorm(const void* x, int in_is_bf16, int rows, int D, const float* gamma,
                      const float* beta, void* out, int out_is_bf16, int perm, int T, int Nsp,
                      const float* add, hipStream_t s, float* out_rs = nullptr);
+// f32 (in_dtype 0) / uint8 (2, normalised /255) frames -> bf16 frames, n values, the patchify kernels'
+// per-value conversion (for the fused patch embedding)
+hipError_t video_to_bf16(const void* video, int in_dtype, bf16_t* out, int64_t n, hipStream_t s);
 // fp32 -> bf16 cast (weights are pre-packed on the host; this is for activations)
 hipError_t cast_f32_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t s);
 // per-token padding vector expansion: frame_pad [B*T] -> token pads in both orders

@@ -139,6 +139,8 @@ _SIGNATURES = {
                                c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "vp_dev_patch_embed": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
     "vp_dev_gemm_tattn": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
@@ -321,6 +323,14 @@ def dev_gemm_tattn(which, a, w, bias, ln_rs, ln_c, out, heads, cap, p=None, stre
     M, K = a.shape
     call("vp_dev_gemm_tattn", which, _ptr(a), _ptr(w), M, K, _ptr(out), _ptr(bias), _ptr(ln_rs), _ptr(ln_c),
          _ptr(p), heads, float(cap), _stream(stream))
+    return out
+
+
+def dev_patch_embed(video, P, wv, bias, pos, out, stream=None):
+    """Fused patch embedding (EPI_POS_BF16) straight from bf16 frames [F, 16P, 16P, 3]."""
+    frames = video.shape[0]
+    call("vp_dev_patch_embed", _ptr(video), frames, P, _ptr(wv), wv.shape[0], _ptr(bias), _ptr(pos), _ptr(out),
+         _stream(stream))
     return out
 
 
