@@ -1,0 +1,14 @@
+// A/B builds of the auxiliary (4096-token) attention kernel (videoprism-mlx_amd/csrc/
+// attention_long_kernel.h) for the tools' diag library: var 0 = the product kernel, 1 = the
+// polynomial numerator in scalar instead of packed fp32 (bitwise the same output).
+#include "attention_long_kernel.h"
+
+extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int64_t num_seq, int64_t S,
+                                         int64_t heads, float cap, void* stream) {
+  using namespace vp;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e = hipErrorInvalidValue;
+  if (var == 0) e = launch_attn_long<0>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 1) e = launch_attn_long<1>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  return e == hipSuccess ? 0 : -1;
+}

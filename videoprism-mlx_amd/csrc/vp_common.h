@@ -80,23 +80,37 @@ inline CapPoly make_cap_poly(float cap) {
                  (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap};
 }
 
+// PACKED: the polynomial in pairs of packed fp32 (v_pk_mul_f32 / v_pk_fma_f32), else scalar fp32
+// (the same IEEE operations per value, so bitwise the same result; packed fp32 VALU beside another
+// wave's MFMAs is priced as an anti-lever in MI355X_MICROARCH.md's price list)
+template <bool PACKED = true>
 __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
   float mx = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
   if (__builtin_amdgcn_ballot_w64(mx > cp.x0) == 0) {
-    // pairs in packed fp32 (v_pk_mul_f32 / v_pk_fma_f32)
-    typedef float f2_t __attribute__((ext_vector_type(2)));
+    if constexpr (PACKED) {
+      typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      const f2_t xv = {x[i], x[i + 1]};
-      const f2_t u = xv * xv;
-      f2_t P = __builtin_elementwise_fma(f2_t(cp.k3), u, f2_t(cp.k2));
-      P = __builtin_elementwise_fma(P, u, f2_t(cp.k1));
-      P = __builtin_elementwise_fma(P, u, f2_t(cp.k0));
-      const f2_t g = xv * P;
-      p[i] = __builtin_amdgcn_exp2f(g.x);
-      p[i + 1] = __builtin_amdgcn_exp2f(g.y);
+      for (int i = 0; i < 16; i += 2) {
+        const f2_t xv = {x[i], x[i + 1]};
+        const f2_t u = xv * xv;
+        f2_t P = __builtin_elementwise_fma(f2_t(cp.k3), u, f2_t(cp.k2));
+        P = __builtin_elementwise_fma(P, u, f2_t(cp.k1));
+        P = __builtin_elementwise_fma(P, u, f2_t(cp.k0));
+        const f2_t g = xv * P;
+        p[i] = __builtin_amdgcn_exp2f(g.x);
+        p[i + 1] = __builtin_amdgcn_exp2f(g.y);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float u = x[i] * x[i];
+        float P = fmaf(cp.k3, u, cp.k2);
+        P = fmaf(P, u, cp.k1);
+        P = fmaf(P, u, cp.k0);
+        p[i] = __builtin_amdgcn_exp2f(x[i] * P);
+      }
     }
   } else {
 #pragma unroll
