@@ -6,7 +6,7 @@ sources are in git history.)"""
 import os
 import sys
 
-if os.environ.get("QH"):
+if os.environ.get("QH") or sys.argv[1:2] == ["long"]:
     os.environ.setdefault("VP_DIAG_LIB", "1")  # the half-frame kernel lives in the diag library
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
