@@ -17,7 +17,8 @@ Also reported (one JSON line on rank 0):
   roofline     the dominant kernel's algorithmic FLOP (or byte) rate, from HIP events recorded
                on its launch stream inside the timed region, against the MI355X dense peak; its
                HBM `traffic` from a PMC record of the same kernel symbol and the same sources
-               (profiles/traffic_r03_<workload>.json, tools/pmc_traffic.sh), else null
+               (the newest profiles/traffic_r*_<workload>.json whose source fingerprint matches,
+               tools/pmc_traffic.sh), else null
   cpu_baseline the NumPy oracle (oracle/, fp32) on one clip on this host's cores (rank 0, N=1)
 
 `--standin` replaces the GPU forward by a small CPU function (gloo backend) so the multi-process
@@ -28,6 +29,7 @@ exercised on a machine without GPUs (tests/test_distributed_cpu.py).  It measure
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import socket
@@ -250,7 +252,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--traffic", default=None,
-                    help="PMC traffic record (default profiles/traffic_r03_<workload>.json)")
+                    help="PMC traffic record (default: the newest profiles/traffic_r*_<workload>.json "
+                         "measured on these sources)")
     ap.add_argument("--standin", action="store_true",
                     help="CPU stand-in forward over gloo: multi-process plumbing test, no measurement")
     ap.add_argument("--spawn-timeout", type=float, default=1200.0,
@@ -402,8 +405,14 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
                      sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
         dom = prof[dom_name]
         avg_s = dom["ms"] / dom["launches"] / 1e3
-        tpath = args.traffic or os.path.join(ROOT, "profiles", f"traffic_r03_{args.workload}.json")
-        traffic, tsrc = load_traffic(tpath, dom_symbol, args.workload, _native.source_fingerprint())
+        fp = _native.source_fingerprint()
+        traffic, tsrc = None, None
+        for tpath in ([args.traffic] if args.traffic else
+                      sorted(glob.glob(os.path.join(ROOT, "profiles", f"traffic_r*_{args.workload}.json")),
+                             reverse=True)):
+            traffic, tsrc = load_traffic(tpath, dom_symbol, args.workload, fp)
+            if traffic is not None:
+                break
         if dom["flops"] > 0:
             ach = dom["flops"] / dom["launches"] / avg_s / 1e12
             roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
