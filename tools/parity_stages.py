@@ -42,13 +42,71 @@ def rest_of_video_path(params, cfg, feats, nm):
     return x, pooled_ln, orc.l2_normalize(pooled_ln)
 
 
+def base_stages(args):
+    """Full Base, B=1, T=8, normal(0, 0.1) frames (tests/test_gpu_encoder.py
+    test_full_base_b1_bf16_vs_oracle): the build-defined pooled vector (token mean + L2) split into the
+    spatial half (GPU spatial_features vs fp64) and the temporal half (the oracle's fp64 temporal stack
+    replayed from the GPU's spatial features)."""
+    import torch
+
+    from oracle import videoprism_oracle as orc
+    from videoprism import models, params
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    var = params.synthetic_params(cfg, seed=0)
+    video = np.random.default_rng(9).normal(0.0, 0.1, (1, 8, 288, 288, 3)).astype(np.float32)
+    mdl = models.get_model("videoprism_public_v1_base", fprop_dtype=torch.bfloat16)
+    emb, out = mdl.apply(var, video, train=False, return_intermediate=["spatial_features"])
+    p = var["params"]
+    ref, rout = orc.factorized_encoder(p, video, cfg, mode="f64", return_intermediate=["spatial_features"])
+    emu, _ = orc.factorized_encoder(p, video, cfg, mode="bf16")
+
+    def pool(e):
+        m = np.asarray(e, np.float64).mean(axis=1)
+        return m / np.sqrt((m * m).sum(-1, keepdims=True) + 1e-12)
+
+    # temporal half of factorized_encoder (oracle lines after spatial_ln), from given spatial features
+    def temporal_from(spf):
+        nm = orc.Numerics("f64")
+        b, t, n, D = 1, 8, 256, cfg["model_dim"]
+        f = np.asarray(spf, np.float64).reshape(b, t, n, D).transpose(0, 2, 1, 3).reshape(b * n, t, D)
+        t_emb = np.asarray(p["temporal_pos_emb"]["emb_var"], np.float64)[:cfg["pos_emb_shape"][0]][None]
+        if t_emb.shape[1] != t:
+            t_emb = orc.interpolate_emb_1d(t_emb, t)
+        f = f + t_emb
+        f = orc.stacked_transformer(f, None, p["temporal_encoder"]["transformers_stack"], nm,
+                                    cfg["num_temporal_layers"], cfg["num_heads"], cfg.get("atten_logit_cap", 0.0))
+        f = orc.layer_norm(f, p["temporal_ln"]["scale"], p["temporal_ln"]["bias"], nm)
+        return f.reshape(b, n, t, D).transpose(0, 2, 1, 3).reshape(b, t * n, D)
+
+    rep = temporal_from(out["spatial_features"])
+    sp_err = np.abs(np.asarray(out["spatial_features"], np.float64) - rout["spatial_features"])
+    rec = {
+        "model": "videoprism_v1_base", "frames": 8,
+        "pooled_vs_f64": float(np.abs(pool(emb) - pool(ref)).max()),
+        "reference_bf16_emulation_pooled_vs_f64": float(np.abs(pool(emu) - pool(ref)).max()),
+        "spatial_features": {"max": float(sp_err.max()), "mean": float(sp_err.mean())},
+        "pooled_from_gpu_spatial_vs_f64": float(np.abs(pool(rep) - pool(ref)).max()),
+        "pooled_gpu_vs_replay": float(np.abs(pool(emb) - pool(rep)).max()),
+        "tokens_vs_f64": {"max": float(np.abs(emb - ref).max()), "mean": float(np.abs(emb - ref).mean())},
+    }
+    print(json.dumps(rec, indent=1), flush=True)
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="videoprism_lvt_v1_base")
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--seed", type=int, default=11)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--base", action="store_true", help="the FactorizedEncoder Base T=8 pooled case instead")
     args = ap.parse_args()
+    if args.base:
+        rec = base_stages(args)
+        if args.json:
+            with open(args.json, "w") as f:
+                json.dump(rec, f, indent=1)
+        return
 
     import torch
 
