@@ -67,18 +67,23 @@ class Numerics:
     mode 'bf16' : float32 arithmetic, activations/params rounded to bf16 at the
                   points where Flax-bf16 stores bf16 (models.py:301-302); softmax
                   stays fp32 (layers.py:650-654).
+    mode 'wbf16': float64 arithmetic on bf16-rounded parameters only: the part of the bf16
+                  mode's deviation from fp64 that the parameter cast alone causes (not a
+                  reference mode -- a parity-analysis tool).
     """
 
     def __init__(self, mode: str = "f64"):
-        assert mode in ("f64", "f32", "bf16"), mode
+        assert mode in ("f64", "f32", "bf16", "wbf16"), mode
         self.mode = mode
-        self.dt = np.float64 if mode == "f64" else np.float32
+        self.dt = np.float32 if mode in ("f32", "bf16") else np.float64
 
     def act(self, x):
         x = np.asarray(x, dtype=self.dt)
         return round_bf16(x) if self.mode == "bf16" else x
 
     def param(self, p):
+        if self.mode == "wbf16":
+            return round_bf16(np.asarray(p, dtype=np.float64))
         return self.act(p)
 
 
@@ -152,7 +157,7 @@ def dot_atten(q, k, v, mask, nm: Numerics, cap: float, dim_per_head: int):
     if cap and cap > 0.0:
         capv = nm.act(cap)
         logits = nm.act(capv * nm.act(np.tanh(nm.act(logits / capv))))
-    sm_dt = np.float64 if nm.mode == "f64" else np.float32  # softmax always >= fp32
+    sm_dt = np.float64 if nm.mode in ("f64", "wbf16") else np.float32  # softmax always >= fp32
     logits = logits.astype(sm_dt)
     if mask is not None:
         logits = apply_mask_to_logits(logits, mask).astype(sm_dt)
@@ -440,7 +445,7 @@ def atten_token_pooling(tokens, p, nm: Numerics, num_heads: int, hidden_dim: int
     qt = np.transpose(q, (0, 2, 1, 3))
     kt = np.transpose(k, (0, 2, 3, 1))
     logits = nm.act(np.matmul(qt, kt))
-    sm_dt = np.float64 if nm.mode == "f64" else np.float32
+    sm_dt = np.float64 if nm.mode in ("f64", "wbf16") else np.float32
     probs = nm.act(softmax(logits.astype(sm_dt)))
     enc = nm.act(np.matmul(probs, np.transpose(v, (0, 2, 1, 3))))
     enc = np.transpose(enc, (0, 2, 1, 3))                                       # [B,1,N,dh]

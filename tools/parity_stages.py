@@ -59,6 +59,7 @@ def base_stages(args):
     p = var["params"]
     ref, rout = orc.factorized_encoder(p, video, cfg, mode="f64", return_intermediate=["spatial_features"])
     emu, _ = orc.factorized_encoder(p, video, cfg, mode="bf16")
+    wq, _ = orc.factorized_encoder(p, orc.round_bf16(video), cfg, mode="wbf16")
 
     def pool(e):
         m = np.asarray(e, np.float64).mean(axis=1)
@@ -84,6 +85,8 @@ def base_stages(args):
         "model": "videoprism_v1_base", "frames": 8,
         "pooled_vs_f64": float(np.abs(pool(emb) - pool(ref)).max()),
         "reference_bf16_emulation_pooled_vs_f64": float(np.abs(pool(emu) - pool(ref)).max()),
+        "bf16_params_and_frames_only_pooled_vs_f64": float(np.abs(pool(wq) - pool(ref)).max()),
+        "pooled_vs_bf16_params_oracle": float(np.abs(pool(emb) - pool(wq)).max()),
         "spatial_features": {"max": float(sp_err.max()), "mean": float(sp_err.mean())},
         "pooled_from_gpu_spatial_vs_f64": float(np.abs(pool(rep) - pool(ref)).max()),
         "pooled_gpu_vs_replay": float(np.abs(pool(emb) - pool(rep)).max()),
@@ -132,6 +135,9 @@ def main():
     aux_rep, pooled_rep, v_rep = rest_of_video_path(p, cfg, st_gpu, nm)
     # the oracle's emulation of the reference's own bf16 graph, for scale
     rv_bf, _, _ = orc.video_clip(p, cfg, video, mode="bf16")
+    # fp64 arithmetic on the bf16-rounded parameters and frames: what the bf16 mode's parameter / input
+    # cast alone costs (the floor any bf16 implementation of the reference shares)
+    rv_w, _, _ = orc.video_clip(p, cfg, orc.round_bf16(video), mode="wbf16")
 
     def mx(a, b):
         return float(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)).max())
@@ -141,6 +147,8 @@ def main():
         "model": args.model, "frames": args.frames, "seed": args.seed,
         "video_emb_vs_f64": mx(v_gpu, rv),
         "reference_bf16_emulation_vs_f64": mx(rv_bf, rv),
+        "bf16_params_and_frames_only_vs_f64": mx(rv_w, rv),
+        "video_emb_vs_bf16_params_oracle": mx(v_gpu, rv_w),
         "vision_tokens": {"max": float(tok_err.max()), "mean": float(tok_err.mean()),
                           "rel_rms": float(np.sqrt((tok_err ** 2).mean() / (st_ref ** 2).mean()))},
         "aux_tokens_from_gpu_vision": {"max": mx(aux_rep, aux_ref),
