@@ -20,4 +20,16 @@ hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const
   return hipErrorInvalidValue;
 }
 
+// the fused temporal attention launches (which 0: EPI_QK_TATTN_LN, 1: EPI_V_TATTN_LN) with ABL bits
+// (16: scalar LN fold -- bitwise equal to the product build)
+hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
+                                  const EpiArgs& ep, hipStream_t s) {
+  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
+  if (which == 0 && abl == 0) return launch_w4<EPI_QK_TATTN_LN, false, true, 0>(A, K, W, K, M, N, K, ep, s);
+  if (which == 0 && abl == 16) return launch_w4<EPI_QK_TATTN_LN, false, true, 16>(A, K, W, K, M, N, K, ep, s);
+  if (which == 1 && abl == 0) return launch_w4<EPI_V_TATTN_LN, false, true, 0>(A, K, W, K, M, N, K, ep, s);
+  if (which == 1 && abl == 16) return launch_w4<EPI_V_TATTN_LN, false, true, 16>(A, K, W, K, M, N, K, ep, s);
+  return hipErrorInvalidValue;
+}
+
 }  // namespace vp

@@ -22,6 +22,21 @@ int vp_dev_gemm_w4_abl(int abl, int s3, const void* A, const void* W, int64_t M,
   return VP_OK;
 }
 
+// the fused temporal attention launches with ablation bits (vp_dev_gemm_tattn of the product ABI + abl)
+int vp_dev_gemm_tattn_abl(int which, int abl, const void* A, const void* W, int64_t M, int64_t K, void* out,
+                          const float* bias, const float* ln_rs, const float* ln_c, const void* p, int64_t heads,
+                          float cap, void* stream) {
+  using namespace vp;
+  EpiArgs ep;
+  ep.out = out; ep.ldo = K; ep.bias = bias; ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.resid = p;
+  ep.cap = cap; ep.heads = (int)heads;
+  ep.cap_c1 = 2.0f * 1.4426950408889634f / cap;
+  ep.cap_c2 = cap * 1.4426950408889634f;
+  VP_HIP(gemm_bf16_w4_tattn_abl(which, abl, (const bf16_t*)A, (const bf16_t*)W, (int)M, (int)(which == 0 ? 2 * K : K),
+                                (int)K, ep, static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // the overlapped-epilogue GEMM (gemm_bf16_ov.hip) with the plain bf16-output epilogues
 int vp_dev_gemm_ov(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
                    const float* bias, const void* resid, void* stream) {

@@ -8,6 +8,7 @@ known-good reference on the same device and data (no epilogue on the torch side)
   python tools/gemm_bench.py fold       # LN-folded / row-statistics epilogues vs the plain ones
   python tools/gemm_bench.py msize      # the FFN GEMMs at smaller M (Infinity-Cache resident A)
   python tools/gemm_bench.py w8b        # 8-wave kernel with the 4-wave pipeline vs the 4-wave one
+  python tools/gemm_bench.py tattn      # fused temporal attention launches: packed vs scalar LN fold
 (Round-1..3 experiments -- early loads, prefetch distances, start skew, tile orders, XCD pairs,
 plain stores -- are recorded in DESIGN.md §4 with their numbers; their builds are in git history.)
 """
@@ -175,11 +176,45 @@ def w8b_ab(dev, g):
         del a, w, o1, o2
 
 
+def tattn(dev, g):
+    """The fused temporal attention launches at the bench shape (M = 131072, D = 768, 12 heads): product
+    build vs the scalar LN-fold build (diag ABL 16), bitwise check, interleaved rounds."""
+    M, D, H = M_TOK, 768, 12
+    x = (torch.rand((M, D), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand((3 * D, D), generator=g, device=dev) * 2 - 1) / D ** 0.5).to(torch.bfloat16)
+    b = torch.zeros(3 * D, device=dev)
+    c = torch.zeros(3 * D, device=dev)
+    rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
+    p = torch.empty(M // 16 * H * 256, device=dev, dtype=torch.bfloat16)
+    o = {0: torch.empty(M, D, device=dev, dtype=torch.bfloat16), 16: torch.empty(M, D, device=dev, dtype=torch.bfloat16)}
+    pp = {0: torch.empty_like(p), 16: torch.empty_like(p)}
+    st = lambda: torch.cuda.current_stream().cuda_stream
+    wv = w[2 * D:].contiguous()
+    def qk(abl):
+        nat.call("vp_dev_gemm_tattn_abl", 0, abl, x.data_ptr(), w.data_ptr(), M, D, pp[abl].data_ptr(), b.data_ptr(),
+                 rs.data_ptr(), c.data_ptr(), None, H, 50.0, st())
+    def vv(abl):
+        nat.call("vp_dev_gemm_tattn_abl", 1, abl, x.data_ptr(), wv.data_ptr(), M, D, o[abl].data_ptr(), b.data_ptr(),
+                 rs.data_ptr(), c.data_ptr(), pp[abl].data_ptr(), H, 50.0, st())
+    for a in (0, 16):
+        qk(a)
+        vv(a)
+    torch.cuda.synchronize()
+    print("tattn scalar == packed (bitwise): P", bool(torch.equal(pp[0], pp[16])), "O", bool(torch.equal(o[0], o[16])),
+          flush=True)
+    fns = {"qk-packed": lambda: qk(0), "qk-scalar": lambda: qk(16), "v-packed": lambda: vv(0), "v-scalar": lambda: vv(16)}
+    res = {k: [] for k in fns}
+    for _ in range(3):
+        for k, f in fns.items():
+            res[k].append(timeit(f))
+    print("tattn:", " | ".join(f"{k} {min(v)*1e3:7.1f} us" for k, v in res.items()), flush=True)
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab}
+    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn}
     modes.get(mode, compare)(dev, g)
 
 

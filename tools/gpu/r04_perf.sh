@@ -11,6 +11,7 @@ step() { local n=$1 t=$2; shift 2; echo "[$(date +%T)] $n start"; timeout -k 10 
 step bench_large 300 bash -c "python -u bench.py --workload large --no-cpu-baseline > gpurun_out/${T}_bench_large.log 2>&1"
 step bench_lvt 400 bash -c "python -u bench.py --workload lvt_large > gpurun_out/${T}_bench_lvt_large.log 2>&1"
 step attn_long 200 bash -c "python -u tools/attn_bench.py long > gpurun_out/${T}_attn_long.log 2>&1"
+step tattn 200 bash -c "VP_DIAG_LIB=1 python -u tools/gemm_bench.py tattn > gpurun_out/${T}_tattn.log 2>&1"
 step stages_base 300 bash -c "python -u tools/parity_stages.py --base --json gpurun_out/${T}_stages_base.json > gpurun_out/${T}_stages_base.log 2>&1"
 step pmc_base 600 bash tools/pmc_traffic.sh gpurun_out/${T}_pmc_base base
 cp profiles/traffic_r04_base.json gpurun_out/ 2>/dev/null

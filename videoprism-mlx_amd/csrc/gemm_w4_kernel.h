@@ -85,7 +85,24 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
-// accumulators stay live).
+// accumulators stay live); 16 = the fused temporal epilogues' LN fold in scalar instead of packed fp32
+// (bitwise equal; packed fp32 VALU beside MFMAs is an anti-lever in MI355X_MICROARCH.md's price list).
+
+// the LN fold of 4 accumulator values (r * a + (m * c + b)), in packed pairs or (SCALAR, diag A/B
+// builds) one fp32 fma at a time -- the same two IEEE fmas per value either way, so bitwise equal
+template <bool SCALAR>
+__device__ __forceinline__ void fold4(const f32x4& a, float r, float m, const float4& c, const float4& b, f32x2_t& lo,
+                                      f32x2_t& hi) {
+  if constexpr (SCALAR) {
+    lo = f32x2_t{fmaf(r, a[0], fmaf(m, c.x, b.x)), fmaf(r, a[1], fmaf(m, c.y, b.y))};
+    hi = f32x2_t{fmaf(r, a[2], fmaf(m, c.z, b.z)), fmaf(r, a[3], fmaf(m, c.w, b.w))};
+  } else {
+    const f32x2_t rr = f32x2_t(r), mm = f32x2_t(m);
+    lo = __builtin_elementwise_fma(rr, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(mm, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
+    hi = __builtin_elementwise_fma(rr, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(mm, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
+  }
+}
+
 template <int EPI, bool NOPAD, bool S3, int ABL = 0, bool AVID = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const bf16_t* __restrict__ A, int64_t lda, const bf16_t* __restrict__ W, int64_t ldw, int M,
@@ -408,13 +425,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
                 uint32_t u[4];
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                  const f32x4& a = acc[hh * 4 + 2 * kk + i][mt];
-                  const float4 c = cc[2 * hh + i], b = bb[2 * hh + i];
-                  const f32x2_t r = f32x2_t(rsA[ml].x), m = f32x2_t(rsA[ml].y);
-                  const f32x2_t lo = __builtin_elementwise_fma(
-                      r, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(m, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
-                  const f32x2_t hi = __builtin_elementwise_fma(
-                      r, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(m, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
+                  f32x2_t lo, hi;
+                  fold4<(ABL & 16) != 0>(acc[hh * 4 + 2 * kk + i][mt], rsA[ml].x, rsA[ml].y, cc[2 * hh + i],
+                                         bb[2 * hh + i], lo, hi);
                   u[2 * i] = pack_bf16x2(lo.x, lo.y);
                   u[2 * i + 1] = pack_bf16x2(hi.x, hi.y);
                 }
@@ -488,7 +501,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           for (int mt = 0; mt < 8; ++mt) {
             char* vb = scr + (mt & 1) * 2048;  // double-buffered V block (16 rows x 64 bf16)
             const bf16x4 pb = pb_n;
-            const f32x2_t r = f32x2_t(rs_n.x), m = f32x2_t(rs_n.y);
+            const float r = rs_n.x, m = rs_n.y;
             if (mt < 7 || nh == 0) {
               pb_n = ld_p((mt + 1) & 7, nh + (mt == 7));
               rs_n = ld_rs((mt + 1) & 7);
@@ -498,11 +511,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
               const int cofs = 4 * (nh * 64 + 16 * q + 4 * g4);
               const float4 c = *reinterpret_cast<const float4*>(lc + cofs);
               const float4 b = *reinterpret_cast<const float4*>(lc + 512 + cofs);
-              const f32x4& a = acc[nh * 4 + q][mt];
-              const f32x2_t lo = __builtin_elementwise_fma(
-                  r, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(m, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
-              const f32x2_t hi = __builtin_elementwise_fma(
-                  r, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(m, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
+              f32x2_t lo, hi;
+              fold4<(ABL & 16) != 0>(acc[nh * 4 + q][mt], r, m, c, b, lo, hi);
               *reinterpret_cast<uint2*>(vb + vunit(r16, 4 * q + g4)) =
                   make_uint2(pack_bf16x2(lo.x, lo.y), pack_bf16x2(hi.x, hi.y));
             }
