@@ -38,3 +38,21 @@ def test_apply_u8_bitwise_equals_normalised_float(cuda, bf16):
     e8, _ = m.apply(var, v)
     ef, _ = m.apply(var, v.astype(np.float32) / np.float32(255.0))
     np.testing.assert_array_equal(e8, ef)
+
+
+def test_apply_three_input_dtypes_bitwise_bf16(cuda):
+    """bf16 forward on the 16 x 16 patch grid: the patch embedding reads bf16 frames directly
+    (gemm_bf16_w4_video); f32 and uint8 frames are converted to bf16 frames first with the patchify
+    kernels' per-value conversion.  All three input dtypes give bitwise the same embedding."""
+    cfg = dict(models.CONFIGS["videoprism_v1_base"])
+    cfg.update(num_spatial_layers=1, num_temporal_layers=1)
+    var = params.synthetic_params(cfg, seed=3)
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedEncoder(**cfg), fprop_dtype=torch.bfloat16)
+    v8 = _frames(2, 2, 4)
+    vf = v8.astype(np.float32) / np.float32(255.0)
+    vb = torch.from_numpy(vf).to(cuda).to(torch.bfloat16)
+    e8, _ = m.apply(var, v8)
+    ef, _ = m.apply(var, vf)
+    eb, _ = m.apply(var, vb)
+    np.testing.assert_array_equal(e8, ef)
+    np.testing.assert_array_equal(ef, eb.float().cpu().numpy() if torch.is_tensor(eb) else eb)
