@@ -523,5 +523,9 @@ def test_patch_embed_fused_from_frames(cuda, frames):
     pt = orc.image_to_patch(v.double().numpy(), P).reshape(-1, P * P * 3)
     ref = pt @ kb.double().numpy() + b.double().numpy() + np.tile(pos.double().numpy(), (frames, 1))
     f, t = fused.double().cpu().numpy(), two.double().cpu().numpy()
-    assert np.all(np.abs(f - t) <= 2 ** -8 * np.abs(ref) + 1e-5), np.abs(f - t).max()
-    assert np.all(np.abs(f - ref) <= 2 ** -8 * np.abs(ref) + 1e-5), np.abs(f - ref).max()
+    # two fp32 sums rounded to bf16 independently: at most one bf16 ulp apart (2^-7 relative just above
+    # a power of two); each within half an ulp of fp64 plus the fp32 summation error
+    assert np.all(np.abs(f - t) <= 2 ** -7 * np.abs(ref) + 1e-5), np.abs(f - t).max()
+    assert np.all(np.abs(f - ref) <= 2 ** -8 * np.abs(ref) + 1e-4), np.abs(f - ref).max()
+    print(f"fused patch embedding, {frames} frames: vs two-kernel max {np.abs(f - t).max():.3e} "
+          f"(mean {np.abs(f - t).mean():.2e}); vs fp64 max {np.abs(f - ref).max():.3e}")
