@@ -32,4 +32,19 @@ hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf1
   return hipErrorInvalidValue;
 }
 
+// the residual-stream epilogues with row statistics (EPI_RESID_BF16_ST: post, EPI_RESID_FFN_BF16_ST:
+// ffn_layer2; S3 as in the product dispatch) with ABL bits (32: block 0's residual rows requested in
+// the tile's last h1 -- bitwise equal to the product build)
+hipError_t gemm_bf16_w4_resid_abl(int epi, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
+                                  const EpiArgs& ep, hipStream_t s) {
+  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
+  if (epi == EPI_RESID_BF16_ST && abl == 0) return launch_w4<EPI_RESID_BF16_ST, false, true, 0>(A, K, W, K, M, N, K, ep, s);
+  if (epi == EPI_RESID_BF16_ST && abl == 32) return launch_w4<EPI_RESID_BF16_ST, false, true, 32>(A, K, W, K, M, N, K, ep, s);
+  if (epi == EPI_RESID_FFN_BF16_ST && abl == 0)
+    return launch_w4<EPI_RESID_FFN_BF16_ST, false, true, 0>(A, K, W, K, M, N, K, ep, s);
+  if (epi == EPI_RESID_FFN_BF16_ST && abl == 32)
+    return launch_w4<EPI_RESID_FFN_BF16_ST, false, true, 32>(A, K, W, K, M, N, K, ep, s);
+  return hipErrorInvalidValue;
+}
+
 }  // namespace vp

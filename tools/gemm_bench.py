@@ -9,6 +9,8 @@ known-good reference on the same device and data (no epilogue on the torch side)
   python tools/gemm_bench.py msize      # the FFN GEMMs at smaller M (Infinity-Cache resident A)
   python tools/gemm_bench.py w8b        # 8-wave kernel with the 4-wave pipeline vs the 4-wave one
   python tools/gemm_bench.py tattn      # fused temporal attention launches: packed vs scalar LN fold
+  python tools/gemm_bench.py early      # post / ffn_layer2 (residual + statistics epilogues): block 0's
+                                        # residual rows requested in the last K-tile vs at the epilogue
 (Round-1..3 experiments -- early loads, prefetch distances, start skew, tile orders, XCD pairs,
 plain stores -- are recorded in DESIGN.md §4 with their numbers; their builds are in git history.)
 """
@@ -210,11 +212,38 @@ def tattn(dev, g):
     print("tattn:", " | ".join(f"{k} {min(v)*1e3:7.1f} us" for k, v in res.items()), flush=True)
 
 
+def early(dev, g):
+    """post (EPI_RESID_BF16_ST) and ffn_layer2 (EPI_RESID_FFN_BF16_ST) at the bench shape: product build vs
+    the build that requests the epilogue's first residual rows in the tile's last h1 (diag ABL 32),
+    bitwise check (the residual is updated in place, so each run starts from the same x), interleaved."""
+    for name, N, K, epi in (("post", 768, 768, nat.EPI_RESID_BF16_ST), ("ffn2", 768, 3072, nat.EPI_RESID_FFN_BF16_ST)):
+        M = M_TOK
+        a, w, b = operands(M, N, K, g, dev)
+        x0 = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16)
+        part = {k: torch.empty((N // 128, M, 2), device=dev) for k in (0, 32)}
+        o = {k: x0.clone() for k in (0, 32)}
+        st = lambda: torch.cuda.current_stream().cuda_stream
+        run = lambda k: nat.call("vp_dev_gemm_resid_abl", epi, k, a.data_ptr(), w.data_ptr(), M, N, K, o[k].data_ptr(),
+                                 b.data_ptr(), part[k].data_ptr(), st())
+        for k in (0, 32):
+            run(k)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(o[0], o[32])) and bool(torch.equal(part[0], part[32]))
+        res = {k: [] for k in (0, 32)}
+        for _ in range(3):
+            for k in (0, 32):
+                res[k].append(timeit(lambda: run(k)))
+        flop = 2.0 * M * N * K
+        print(f"{name} early residual == product (bitwise): {same}: " + " | ".join(
+            f"abl{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
+        del a, x0, o, part
+
+
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn}
+    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn, "early": early}
     modes.get(mode, compare)(dev, g)
 
 

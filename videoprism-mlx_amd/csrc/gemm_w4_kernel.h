@@ -86,7 +86,9 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
 // accumulators stay live); 16 = the fused temporal epilogues' LN fold in scalar instead of packed fp32
-// (bitwise equal; packed fp32 VALU beside MFMAs is an anti-lever in MI355X_MICROARCH.md's price list).
+// (bitwise equal; packed fp32 VALU beside MFMAs is an anti-lever in MI355X_MICROARCH.md's price list);
+// 32 = the residual rows of the epilogue's first block requested in the tile's last h1 instead of at
+// the epilogue's start (bitwise equal).
 
 // the LN fold of 4 accumulator values (r * a + (m * c + b)), in packed pairs or (SCALAR, diag A/B
 // builds) one fp32 fma at a time -- the same two IEEE fmas per value either way, so bitwise equal
@@ -270,9 +272,22 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     sched_fence();
   };
+  // the epilogue's residual / position rows of block (mt, nh, pass) -> ex[buffer][nh][pass], for the
+  // tile whose wave origin is (m0, n0)
+  const int er = lane >> 3, es = lane & 7;  // epilogue read-back: row pass*8 + er, column segment es
+  F8 ex[2][2][2];
+  int ex_m0 = 0, ex_n0 = 0;  // ABL 32: the current tile's wave origin (set at tile start)
+  auto fetch = [&](int bsel, int mt, int m0, int n0) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass)
+        ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+  };
   // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
-  // 16 loads of K-tile g+2 into buffer cb
-  auto h1 = [&](int cb) {
+  // 16 loads of K-tile g+2 into buffer cb.  last: the tile's last K-tile (ABL 32: block 0's residual
+  // rows are requested there, ahead of the next tile's W pieces)
+  auto h1 = [&](int cb, bool last) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // S3: K-tile g+1 has landed once all but this K-tile's h0 A pieces (of g+2) are done
     if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -283,6 +298,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     sched_fence();
     __builtin_amdgcn_s_barrier();
     sched_fence();
+    if constexpr ((ABL & 32) != 0 && EpiTraits<EPI>::kExtra) {
+      if (last) fetch(0, 0, ex_m0, ex_n0);
+      sched_fence();
+    }
     const int an = a3 == 2 ? 0 : a3 + 1;  // S3: A buffer of K-tile g+1
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -313,7 +332,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   };
 
   int g = 0;
-  const int er = lane >> 3, es = lane & 7;  // epilogue read-back: row pass*8 + er, column segment es
   for (int j = 0; j < count; ++j) {
     // this tile's bias columns, requested before any of the tile's K-stream loads: vmcnt
     // retires in issue order, so a bias load issued in the epilogue would wait for the next
@@ -324,6 +342,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     {
       int ttm, ttn;
       coords(first + j * stride, ttm, ttn);
+      if constexpr ((ABL & 32) != 0) {
+        ex_m0 = ttm * BM + wm * 128;
+        ex_n0 = ttn * BN + wn * 128;
+      }
       const int nb = ttn * BN + wn * 128 + es * 8;
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) {
@@ -345,11 +367,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       }
     }
     h0(g & 1, true);
-    h1(g & 1);
+    h1(g & 1, nk == 1);
     ++g;
     for (int kt = 1; kt < nk; ++kt, ++g) {
       h0(g & 1, false);
-      h1(g & 1);
+      h1(g & 1, kt == nk - 1);
     }
 
     // ---- epilogue of tile j.  acc[nt][mt] holds D[row mb + 16*mt][cols nb + 16*nt + 4*(lane>>4)
@@ -530,14 +552,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)
-    F8 ex[2][2][2];  // [buffer][nh][pass]
-    auto fetch = [&](int bsel, int mt) {
-#pragma unroll
-      for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-        for (int pass = 0; pass < 2; ++pass)
-          ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
-    };
     // block G = (mt, nh): acc[nh*4 + q][mt], q = 0..3 -> scratch buffer G & 1.  Block G+1 is
     // written before block G is read back, so the LDS round trip overlaps the math and stores.
     auto put = [&](int G) {
@@ -553,14 +567,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     // es keeps the partials of mt == es, so the wave stores its 128 rows with 2 instructions
     float sv[2][8];
     float pS[2] = {0.f, 0.f}, pQ[2] = {0.f, 0.f};
-    if constexpr (Tr::kExtra) fetch(0, 0);
+    if constexpr (Tr::kExtra && !(ABL & 32)) fetch(0, 0, m0, n0);
     put(0);
 #pragma unroll
     for (int G = 0; G < 16; ++G) {
       const int mt = G >> 1, nh = G & 1;
       if (G + 1 < 16) put(G + 1);
       if constexpr (Tr::kExtra) {
-        if (nh == 0 && mt < 7) fetch((mt + 1) & 1, mt + 1);
+        if (nh == 0 && mt < 7) fetch((mt + 1) & 1, mt + 1, m0, n0);
       }
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
