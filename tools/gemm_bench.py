@@ -180,7 +180,8 @@ def w8b_ab(dev, g):
 
 def tattn(dev, g):
     """The fused temporal attention launches at the bench shape (M = 131072, D = 768, 12 heads): product
-    build vs the scalar LN-fold build (diag ABL 16), bitwise check, interleaved rounds."""
+    build vs the scalar LN-fold build (diag ABL 16), bitwise check, and the no-epilogue builds (ABL 8,
+    prices the epilogues); interleaved rounds."""
     M, D, H = M_TOK, 768, 12
     x = (torch.rand((M, D), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand((3 * D, D), generator=g, device=dev) * 2 - 1) / D ** 0.5).to(torch.bfloat16)
@@ -204,7 +205,9 @@ def tattn(dev, g):
     torch.cuda.synchronize()
     print("tattn scalar == packed (bitwise): P", bool(torch.equal(pp[0], pp[16])), "O", bool(torch.equal(o[0], o[16])),
           flush=True)
-    fns = {"qk-packed": lambda: qk(0), "qk-scalar": lambda: qk(16), "v-packed": lambda: vv(0), "v-scalar": lambda: vv(16)}
+    pp[8], o[8] = torch.empty_like(p), torch.empty_like(o[0])
+    fns = {"qk-packed": lambda: qk(0), "qk-scalar": lambda: qk(16), "qk-noepi": lambda: qk(8),
+           "v-packed": lambda: vv(0), "v-scalar": lambda: vv(16), "v-noepi": lambda: vv(8)}
     res = {k: [] for k in fns}
     for _ in range(3):
         for k, f in fns.items():
