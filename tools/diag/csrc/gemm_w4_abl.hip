@@ -21,7 +21,8 @@ hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const
 }
 
 // the fused temporal attention launches (which 0: EPI_QK_TATTN_LN, 1: EPI_V_TATTN_LN) with ABL bits
-// (16: scalar LN fold -- bitwise equal to the product build; 8: no epilogue, prices it)
+// (16: scalar LN fold -- bitwise equal to the product build; 8: no epilogue, prices it; 64: V launch
+// loads P 2 steps ahead)
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
                                   const EpiArgs& ep, hipStream_t s) {
   if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
@@ -31,6 +32,7 @@ hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf1
   if (which == 1 && abl == 16) return launch_w4<EPI_V_TATTN_LN, false, true, 16>(A, K, W, K, M, N, K, ep, s);
   if (which == 0 && abl == 8) return launch_w4<EPI_QK_TATTN_LN, false, true, 8>(A, K, W, K, M, N, K, ep, s);
   if (which == 1 && abl == 8) return launch_w4<EPI_V_TATTN_LN, false, true, 8>(A, K, W, K, M, N, K, ep, s);
+  if (which == 1 && abl == 64) return launch_w4<EPI_V_TATTN_LN, false, true, 64>(A, K, W, K, M, N, K, ep, s);
   return hipErrorInvalidValue;
 }
 

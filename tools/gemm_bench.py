@@ -199,15 +199,18 @@ def tattn(dev, g):
     def vv(abl):
         nat.call("vp_dev_gemm_tattn_abl", 1, abl, x.data_ptr(), wv.data_ptr(), M, D, o[abl].data_ptr(), b.data_ptr(),
                  rs.data_ptr(), c.data_ptr(), pp[abl].data_ptr(), H, 50.0, st())
-    for a in (0, 16):
-        qk(a)
+    o[64] = torch.empty_like(o[0])
+    pp[64] = pp[0]
+    for a in (0, 16, 64):
+        if a != 64:
+            qk(a)
         vv(a)
     torch.cuda.synchronize()
     print("tattn scalar == packed (bitwise): P", bool(torch.equal(pp[0], pp[16])), "O", bool(torch.equal(o[0], o[16])),
-          flush=True)
-    pp[8], o[8] = torch.empty_like(p), torch.empty_like(o[0])
+          "| V pf2 == product:", bool(torch.equal(o[0], o[64])), flush=True)
+    pp[8], o[8] = torch.empty_like(p), torch.empty_like(o[0])  # (no-epilogue builds: nothing written)
     fns = {"qk-packed": lambda: qk(0), "qk-scalar": lambda: qk(16), "qk-noepi": lambda: qk(8),
-           "v-packed": lambda: vv(0), "v-scalar": lambda: vv(16), "v-noepi": lambda: vv(8)}
+           "v-packed": lambda: vv(0), "v-scalar": lambda: vv(16), "v-noepi": lambda: vv(8), "v-pf2": lambda: vv(64)}
     res = {k: [] for k in fns}
     for _ in range(3):
         for k, f in fns.items():

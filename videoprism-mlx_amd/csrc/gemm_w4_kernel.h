@@ -88,7 +88,8 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // accumulators stay live); 16 = the fused temporal epilogues' LN fold in scalar instead of packed fp32
 // (bitwise equal; packed fp32 VALU beside MFMAs is an anti-lever in MI355X_MICROARCH.md's price list);
 // 32 = the residual rows of the epilogue's first block requested in the tile's last h1 instead of at
-// the epilogue's start (bitwise equal).
+// the epilogue's start (bitwise equal); 64 = the fused V launch's P / row-statistics loads 2 (sequence,
+// head) steps ahead instead of one (bitwise equal).
 
 // the LN fold of 4 accumulator values (r * a + (m * c + b)), in packed pairs or (SCALAR, diag A/B
 // builds) one fp32 fma at a time -- the same two IEEE fmas per value either way, so bitwise equal
@@ -515,18 +516,26 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           return *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + nh * 64) >> 6)) * 256 + lid * 4);
         };
         auto ld_rs = [&](int mt) { return *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + mt * 16 + r16)); };
-        bf16x4 pb_n = ld_p(0, 0);
-        float2 rs_n = ld_rs(0);
+        // (ABL 64: kVpf = 2 (sequence, head) steps ahead instead of one)
+        constexpr int kVpf = (ABL & 64) ? 2 : 1;
+        bf16x4 pbq[kVpf];
+        float2 rsq[kVpf];
+#pragma unroll
+        for (int st = 0; st < kVpf; ++st) {
+          pbq[st] = ld_p(st & 7, st >> 3);
+          rsq[st] = ld_rs(st & 7);
+        }
 #pragma unroll
         for (int nh = 0; nh < 2; ++nh) {
 #pragma unroll
           for (int mt = 0; mt < 8; ++mt) {
             char* vb = scr + (mt & 1) * 2048;  // double-buffered V block (16 rows x 64 bf16)
-            const bf16x4 pb = pb_n;
-            const float r = rs_n.x, m = rs_n.y;
-            if (mt < 7 || nh == 0) {
-              pb_n = ld_p((mt + 1) & 7, nh + (mt == 7));
-              rs_n = ld_rs((mt + 1) & 7);
+            const int st = nh * 8 + mt, sl = st % kVpf;
+            const bf16x4 pb = pbq[sl];
+            const float r = rsq[sl].x, m = rsq[sl].y;
+            if (st + kVpf < 16) {
+              pbq[sl] = ld_p((st + kVpf) & 7, (st + kVpf) >> 3);
+              rsq[sl] = ld_rs((st + kVpf) & 7);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
