@@ -497,11 +497,10 @@ def test_temporal_attention_fused_kernels_vs_unfused(cuda, heads):
 @pytest.mark.parametrize("frames", [3, 9])
 def test_patch_embed_fused_from_frames(cuda, frames):
     """The fused patch embedding (gemm_bf16_w4_video: the GEMM stages its A tiles straight from the
-    bf16 frames, one K-tile per patch row, no patch tensor) against the two-kernel path
-    (patchify -> [M, 1024] patches -> GEMM) and against fp64 on the same bf16 frames: the sums differ
-    only in their fp32 order, so |fused - two-kernel| <= 2^-8 |ref| + 1e-5, and the fused result is
-    within one bf16 rounding of fp64.  Frames with large values in every patch's neighbours check
-    that the 128-B source windows' overlap into the next patch meets zero weights only."""
+    bf16 frames in 16-B chunks of the patch pixel rows, no patch tensor) against the two-kernel
+    path (patchify -> [M, 1024] patches -> GEMM) and against fp64 on the same bf16 frames: the sums
+    differ only in their fp32 order (at most one bf16 ulp apart), and the fused result is within one
+    bf16 rounding of fp64.  The chunk that overlaps its predecessor must meet zero weights there."""
     P, D = 18, 768
     g = torch.Generator(device="cpu").manual_seed(frames)
     v = _bf(torch.rand(frames, 16 * P, 16 * P, 3, generator=g) * 4 - 1)
@@ -509,9 +508,7 @@ def test_patch_embed_fused_from_frames(cuda, frames):
     kb = _bf(k)
     b = torch.randn(D, generator=g) * 0.1
     pos = torch.randn(256, D, generator=g) * 0.1
-    wv = torch.zeros(D, 64 * P)
-    for py in range(P):
-        wv[:, 64 * py:64 * py + 3 * P] = kb[py * 3 * P:(py + 1) * 3 * P].T
+    wv = nat.video_patch_w(kb, P)
     wk = torch.zeros(D, 1024)
     wk[:, :P * P * 3] = kb.T
     vd = v.to(cuda)

@@ -77,11 +77,13 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // pieces over both phases is.)
 // AVID: A is the video itself (patch embedding without a patch tensor): bf16 frames
 // [frames][16P][16P][3] of a 16x16 patch grid, so a 256-row tile is one frame and a piece's 8 rows
-// are 8 horizontally adjacent patches; K-tile kt is patch row kt (P <= 21: its 3P channels-last
-// values are contiguous and fill the first 6P bytes of the 128-B K-tile row), i.e. K = 64 P with
-// W zero outside columns 64 kt + [0, 3P).  The 128-B source window of a row runs 128 - 6P bytes
-// into the next patch (or the next pixel row); those values meet zero W columns.  lda = the
-// pixel-row length in elements (16 P * 3); the buffer descriptor spans the M / 256 frames.
+// are 8 horizontally adjacent patches.  A patch's pixel row py is 3P contiguous channels-last values;
+// it is read as cpr = ceil(3P / 8) 16-B chunks at value offsets min(8 cr, 3P - 8) (the last chunk
+// overlaps its predecessor instead of running past the row segment), and chunk c = cpr py + cr of the
+// patch fills K columns 8c .. 8c + 7, so K = 64 ceil(P cpr / 8) (P = 18: 126 chunks, K = 1024).  W is
+// zero at the overlap and past the P cpr chunks, whose slots re-read chunk 0.  Each lane's source
+// offset thus depends on the K-tile (video_chunk_off below, a few VALU per K-tile).  lda = the
+// pixel-row length in elements (48 P); the buffer descriptor spans the M / 256 frames.
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
@@ -157,9 +159,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // Lane: row (lane>>3) of the piece, LDS chunk (lane&7) <- source chunk (lane&7)^swz(row);
   // swz(row) of piece i depends only on i & 1.
   const uint32_t a_rb = (uint32_t)(lda * 2), w_rb = (uint32_t)(ldw * 2);
-  // AVID: a_rb = one pixel row of a frame; P = nk pixel rows per patch, 16 P rows per frame
-  const uint32_t prow_b = AVID ? (uint32_t)(6 * (K / BK)) : 0;    // bytes of one patch's pixel row
-  const uint32_t frame_b = AVID ? (uint32_t)(16 * (K / BK)) * a_rb : 0;
+  // AVID: a_rb = one pixel row of a frame (48 P values), 16 P pixel rows per frame; cpr chunks per
+  // patch pixel row, c / cpr = (c * av_mag) >> 16 for the chunk indices of a patch (< 1024 / cpr)
+  const int av_p = AVID ? (int)(lda / 48) : 0;
+  const int av_cpr = AVID ? (3 * av_p + 7) >> 3 : 1;
+  const uint32_t av_mag = AVID ? (65535u + (uint32_t)av_cpr) / (uint32_t)av_cpr : 0;
+  const uint32_t prow_b = AVID ? (uint32_t)(6 * av_p) : 0;    // bytes of one patch's pixel row
+  const uint32_t frame_b = AVID ? (uint32_t)(16 * av_p) * a_rb : 0;
   const uint64_t a_bytes = AVID ? (uint64_t)(M / BM) * frame_b : (uint64_t)M * a_rb;
   const uint64_t w_bytes = (uint64_t)N * w_rb;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)(uint32_t)a_bytes, 0x00020000);
@@ -168,6 +174,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   const uint32_t cE = (uint32_t)((lane & 7) ^ swz(prow)) * 16;       // even pieces
   const uint32_t cO = (uint32_t)((lane & 7) ^ swz(prow + 8)) * 16;   // odd pieces
   const uint32_t vA[2] = {prow * (AVID ? prow_b : a_rb) + cE, prow * (AVID ? prow_b : a_rb) + cO};
+  // AVID: this lane's source offset in K-tile kt for even (par 0) / odd pieces: logical chunk
+  // (lane & 7) ^ swz of the K-tile row = patch chunk c = 8 kt + j
+  auto video_chunk_off = [&](int kt, int par) -> uint32_t {
+    const int c = kt * 8 + ((lane & 7) ^ swz(prow + 8 * par));
+    int py = (int)(((uint32_t)c * av_mag) >> 16);
+    int vo = min(8 * (c - py * av_cpr), 3 * av_p - 8);
+    if (c >= av_p * av_cpr) py = vo = 0;
+    return prow * prow_b + (uint32_t)py * a_rb + (uint32_t)vo * 2;
+  };
   const uint32_t vW[2] = {prow * w_rb + cE, prow * w_rb + cO};
   typedef __attribute__((address_space(3))) void lds_void;
   // load stream: K-tile ld_g -> (tile ld_tm/ld_tn, K-tile ld_kt); the tail re-loads the last
@@ -193,13 +208,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     char* dst = (p >= 8 ? w_buf(buf) : a_buf(buf)) + (w * 8 + i) * 1024;
     if (p < 8) {
       uint32_t so;
+      uint32_t vo = vA[i & 1];
       if constexpr (AVID) {  // piece w*8+i: patch-grid row (w*8+i) >> 1, patches 8 ((w*8+i) & 1) + 0..7
         const int pc = w * 8 + i;
-        so = (uint32_t)ld_tm * frame_b + (uint32_t)((pc >> 1) * (K / BK) + ld_kt) * a_rb + (uint32_t)(pc & 1) * 8 * prow_b;
+        so = (uint32_t)ld_tm * frame_b + (uint32_t)((pc >> 1) * av_p) * a_rb + (uint32_t)(pc & 1) * 8 * prow_b;
+        vo = video_chunk_off(ld_kt, i & 1);
       } else {
         so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vo, so, 0, 0);
     } else {
       const uint32_t so = (uint32_t)(ld_tn * BN + (w * 8 + i) * 8) * w_rb + ld_kt * (BK * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void*)dst, 16, vW[i & 1], so, 0, 0);

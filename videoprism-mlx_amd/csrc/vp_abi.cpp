@@ -116,11 +116,18 @@ int vp_finalize(vp_handle* h) {
     for (int64_t i = 0; i < kreal; ++i)
       for (int64_t n = 0; n < D; ++n) t[(size_t)n * h->kpad + i] = k[(size_t)i * D + n];
     if ((rc = upload_mat(h, t, &h->wpatch))) return rc;
-    if (is_bf16(h) && 3 * P <= 64) {  // one 64-column K-tile per patch row (gemm_bf16_w4_video)
-      std::vector<float> tv((size_t)D * 64 * P, 0.0f);
+    if (is_bf16(h) && P >= 3 && 3 * P <= 64) {  // the frames' chunk order (gemm_bf16_w4_video, vp_kernels.h)
+      const int64_t cpr = vp::video_patch_cpr((int)P), kv = vp::video_patch_k((int)P);
+      std::vector<float> tv((size_t)D * kv, 0.0f);
       for (int64_t py = 0; py < P; ++py)
-        for (int64_t j = 0; j < 3 * P; ++j)
-          for (int64_t n = 0; n < D; ++n) tv[(size_t)n * 64 * P + py * 64 + j] = k[(size_t)(py * 3 * P + j) * D + n];
+        for (int64_t cr = 0; cr < cpr; ++cr) {
+          const int64_t vo = std::min<int64_t>(8 * cr, 3 * P - 8);
+          for (int64_t e = 0; e < 8; ++e) {
+            const int64_t v = vo + e;
+            if (cr == cpr - 1 && v < 8 * (cpr - 1)) continue;  // overlap with the row's previous chunk
+            for (int64_t n = 0; n < D; ++n) tv[(size_t)n * kv + 8 * (py * cpr + cr) + e] = k[(size_t)(py * 3 * P + v) * D + n];
+          }
+        }
       if ((rc = upload_mat(h, tv, &h->wpatch_v))) return rc;
     }
     if ((rc = upload_f32(h, param_data(h, px + "patch_projection/linear/bias"), &h->bpatch))) return rc;
@@ -536,12 +543,12 @@ int vp_dev_gemm_tattn(int which, const void* A, const void* W, int64_t M, int64_
 }
 
 // Not in the public header: the fused patch embedding (gemm_bf16_w4_video, EPI_POS_BF16) for kernel
-// tests: bf16 frames [frames][16P][16P][3], wv [N][64 P] (patch row py at columns 64 py + [0, 3P)),
-// pos [256][N] fp32 -> out [frames*256][N] bf16.
+// tests: bf16 frames [frames][16P][16P][3], wv [N][video_patch_k(P)] in the frames' chunk order
+// (vp_kernels.h), pos [256][N] fp32 -> out [frames*256][N] bf16.
 int vp_dev_patch_embed(const void* video, int64_t frames, int64_t P, const void* wv, int64_t N, const float* bias,
                        const float* pos, void* out, void* stream) {
   using namespace vp;
-  if (!video || !wv || !bias || !pos || !out || frames < 1 || P < 1 || 3 * P > 64 || N % 256)
+  if (!video || !wv || !bias || !pos || !out || frames < 1 || P < 3 || 3 * P > 64 || N % 256)
     return fail(VP_EINVAL, "bad argument");
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.pos = pos; ep.pos_rows = 256;

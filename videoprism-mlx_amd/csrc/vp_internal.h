@@ -137,7 +137,7 @@ struct vp_handle {
   // packed device weights
   int kpad = 0;
   void* wpatch = nullptr;      // [D][kpad]
-  void* wpatch_v = nullptr;    // bf16, 3P <= 64: [D][64 P], patch row py at columns 64 py + [0, 3P) (fused
+  void* wpatch_v = nullptr;    // bf16, 3 <= P <= 21: [D][video_patch_k(P)] in the frames' chunk order (fused
                                // patch embedding straight from the frames, gemm_bf16_w4_video)
   float* bpatch = nullptr;
   float* spatial_pos = nullptr;    // [pos_h*pos_w][D]

@@ -331,6 +331,26 @@ def dev_gemm_tattn(which, a, w, bias, ln_rs, ln_c, out, heads, cap, p=None, stre
     return out
 
 
+def video_patch_w(k, P):
+    """The fused patch embedding's weight layout (vp_kernels.h video_patch_k; packed the same way by
+    vp_finalize): k [P*P*3, N] (the patch kernel) -> [N, K] with patch pixel row py read as
+    cpr = ceil(3P/8) chunks of 8 values at value offsets min(8 cr, 3P - 8), chunk c = cpr py + cr at
+    columns 8c..8c+7, zero where a row's last chunk overlaps its predecessor and past the P cpr chunks."""
+    import torch
+    cpr = (3 * P + 7) // 8
+    kv = (P * cpr + 7) // 8 * 64
+    out = torch.zeros(k.shape[1], kv, dtype=k.dtype)
+    for py in range(P):
+        for cr in range(cpr):
+            vo = min(8 * cr, 3 * P - 8)
+            for e in range(8):
+                v = vo + e
+                if cr == cpr - 1 and v < 8 * (cpr - 1):
+                    continue
+                out[:, 8 * (py * cpr + cr) + e] = k[py * 3 * P + v]
+    return out
+
+
 def dev_patch_embed(video, P, wv, bias, pos, out, stream=None):
     """Fused patch embedding (EPI_POS_BF16) straight from bf16 frames [F, 16P, 16P, 3]."""
     frames = video.shape[0]
