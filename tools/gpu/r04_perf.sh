@@ -8,6 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 T=${1:-r04b}
 step() { local n=$1 t=$2; shift 2; echo "[$(date +%T)] $n start"; timeout -k 10 "$t" "$@"; local rc=$?; echo "[$(date +%T)] $n rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+step tests_patch 300 bash -c "python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_ingest.py tests/test_gpu_fullsize.py -m gpu -x -v -s --timeout 200 --timeout-method thread > gpurun_out/${T}_tests_patch.log 2>&1"
 step bench_large 300 bash -c "python -u bench.py --workload large --no-cpu-baseline > gpurun_out/${T}_bench_large.log 2>&1"
 step bench_lvt 400 bash -c "python -u bench.py --workload lvt_large > gpurun_out/${T}_bench_lvt_large.log 2>&1"
 step attn_long 200 bash -c "python -u tools/attn_bench.py long > gpurun_out/${T}_attn_long.log 2>&1"
