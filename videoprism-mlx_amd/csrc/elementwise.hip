@@ -242,14 +242,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 }
 
 // ---- LayerNorm statistics for the GEMM-folded LayerNorm (EPI_*_LN) ----
-// partials: st[p][row] = (sum, M2) over columns [128p, 128p+128) of the stored bf16 row
-__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ st, int P,
+// partials: st[p][row] = (sum, M2) over columns [128p, 128p+128) of the stored bf16 row.  PP: the
+// partial count as a compile-time constant (D = 768: 6, D = 1024: 8), so the P loads are all in flight
+// at once -- with a run-time count each iteration waited for its load (6 serial memory latencies:
+// 5.3 us per launch, 31 launches per Base step); PP = 0: run-time P
+template <int PP>
+__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ st, int P_rt,
                                                                 int64_t M, float* __restrict__ rs_out) {
+  const int P = PP > 0 ? PP : P_rt;
   const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (row >= M) return;
   float S[16], Q[16];
   float tot = 0.f;
-  for (int p = 0; p < P; ++p) {
+#pragma unroll
+  for (int p = 0; p < (PP > 0 ? PP : 16); ++p) {
+    if (PP == 0 && p >= P) break;
     const float2 v = *reinterpret_cast<const float2*>(st + 2 * ((int64_t)p * M + row));
     S[p] = v.x;
     Q[p] = v.y;
@@ -258,7 +265,9 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __r
   const float D = 128.0f * P;
   const float mean = tot / D;
   float m2 = 0.f;
-  for (int p = 0; p < P; ++p) {  // Chan: M2 = sum Q_p + n_p (mean_p - mean)^2
+#pragma unroll
+  for (int p = 0; p < (PP > 0 ? PP : 16); ++p) {  // Chan: M2 = sum Q_p + n_p (mean_p - mean)^2
+    if (PP == 0 && p >= P) break;
     const float d = S[p] * (1.0f / 128.0f) - mean;
     m2 += Q[p] + 128.0f * d * d;
   }
@@ -447,8 +456,10 @@ hipError_t layernorm(const void* x, int in_is_bf16, int rows, int D, const float
 
 hipError_t ln_stats_finalize(const float* st_part, int P, int64_t M, float* ln_rs, hipStream_t s) {
   if (P < 1 || P > 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, st_part, P, M,
-                     ln_rs);
+  const dim3 g((unsigned)((M + 255) / 256));
+  if (P == 6) hipLaunchKernelGGL(ln_stats_finalize_kernel<6>, g, dim3(256), 0, s, st_part, P, M, ln_rs);
+  else if (P == 8) hipLaunchKernelGGL(ln_stats_finalize_kernel<8>, g, dim3(256), 0, s, st_part, P, M, ln_rs);
+  else hipLaunchKernelGGL(ln_stats_finalize_kernel<0>, g, dim3(256), 0, s, st_part, P, M, ln_rs);
   return hipGetLastError();
 }
 
