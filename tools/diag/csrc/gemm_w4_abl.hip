@@ -21,33 +21,14 @@ hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const
 }
 
 // the fused temporal attention launches (which 0: EPI_QK_TATTN_LN, 1: EPI_V_TATTN_LN) with ABL bits
-// (16: scalar LN fold -- bitwise equal to the product build; 8: no epilogue, prices it; 64: V launch
-// loads P 2 steps ahead)
+// (8: no epilogue, prices it)
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
                                   const EpiArgs& ep, hipStream_t s) {
   if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
   if (which == 0 && abl == 0) return launch_w4<EPI_QK_TATTN_LN, false, true, 0>(A, K, W, K, M, N, K, ep, s);
-  if (which == 0 && abl == 16) return launch_w4<EPI_QK_TATTN_LN, false, true, 16>(A, K, W, K, M, N, K, ep, s);
   if (which == 1 && abl == 0) return launch_w4<EPI_V_TATTN_LN, false, true, 0>(A, K, W, K, M, N, K, ep, s);
-  if (which == 1 && abl == 16) return launch_w4<EPI_V_TATTN_LN, false, true, 16>(A, K, W, K, M, N, K, ep, s);
   if (which == 0 && abl == 8) return launch_w4<EPI_QK_TATTN_LN, false, true, 8>(A, K, W, K, M, N, K, ep, s);
   if (which == 1 && abl == 8) return launch_w4<EPI_V_TATTN_LN, false, true, 8>(A, K, W, K, M, N, K, ep, s);
-  if (which == 1 && abl == 64) return launch_w4<EPI_V_TATTN_LN, false, true, 64>(A, K, W, K, M, N, K, ep, s);
-  return hipErrorInvalidValue;
-}
-
-// the residual-stream epilogues with row statistics (EPI_RESID_BF16_ST: post, EPI_RESID_FFN_BF16_ST:
-// ffn_layer2; S3 as in the product dispatch) with ABL bits (32: block 0's residual rows requested in
-// the tile's last h1 -- bitwise equal to the product build)
-hipError_t gemm_bf16_w4_resid_abl(int epi, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
-                                  const EpiArgs& ep, hipStream_t s) {
-  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
-  if (epi == EPI_RESID_BF16_ST && abl == 0) return launch_w4<EPI_RESID_BF16_ST, false, true, 0>(A, K, W, K, M, N, K, ep, s);
-  if (epi == EPI_RESID_BF16_ST && abl == 32) return launch_w4<EPI_RESID_BF16_ST, false, true, 32>(A, K, W, K, M, N, K, ep, s);
-  if (epi == EPI_RESID_FFN_BF16_ST && abl == 0)
-    return launch_w4<EPI_RESID_FFN_BF16_ST, false, true, 0>(A, K, W, K, M, N, K, ep, s);
-  if (epi == EPI_RESID_FFN_BF16_ST && abl == 32)
-    return launch_w4<EPI_RESID_FFN_BF16_ST, false, true, 32>(A, K, W, K, M, N, K, ep, s);
   return hipErrorInvalidValue;
 }
 

@@ -37,20 +37,6 @@ int vp_dev_gemm_tattn_abl(int which, int abl, const void* A, const void* W, int6
   return VP_OK;
 }
 
-// the residual-stream GEMMs (EPI_RESID_BF16_ST / EPI_RESID_FFN_BF16_ST, residual in place in out) with
-// ablation bits
-int vp_dev_gemm_resid_abl(int epi, int abl, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
-                          const float* bias, float* st_part, void* stream) {
-  using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
-  EpiArgs ep;
-  ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = out; ep.ldr = N; ep.st_part = st_part; ep.st_rows = M;
-  VP_HIP(gemm_bf16_w4_resid_abl(epi, abl, (const bf16_t*)A, (const bf16_t*)W, (int)M, (int)N, (int)K, ep,
-                                static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-
 // the overlapped-epilogue GEMM (gemm_bf16_ov.hip) with the plain bf16-output epilogues
 int vp_dev_gemm_ov(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
                    const float* bias, const void* resid, void* stream) {

@@ -8,9 +8,7 @@ known-good reference on the same device and data (no epilogue on the torch side)
   python tools/gemm_bench.py fold       # LN-folded / row-statistics epilogues vs the plain ones
   python tools/gemm_bench.py msize      # the FFN GEMMs at smaller M (Infinity-Cache resident A)
   python tools/gemm_bench.py w8b        # 8-wave kernel with the 4-wave pipeline vs the 4-wave one
-  python tools/gemm_bench.py tattn      # fused temporal attention launches: packed vs scalar LN fold
-  python tools/gemm_bench.py early      # post / ffn_layer2 (residual + statistics epilogues): block 0's
-                                        # residual rows requested in the last K-tile vs at the epilogue
+  python tools/gemm_bench.py tattn      # fused temporal attention launches vs their no-epilogue builds
 (Round-1..3 experiments -- early loads, prefetch distances, start skew, tile orders, XCD pairs,
 plain stores -- are recorded in DESIGN.md §4 with their numbers; their builds are in git history.)
 """
@@ -180,8 +178,7 @@ def w8b_ab(dev, g):
 
 def tattn(dev, g):
     """The fused temporal attention launches at the bench shape (M = 131072, D = 768, 12 heads): product
-    build vs the scalar LN-fold build (diag ABL 16), bitwise check, and the no-epilogue builds (ABL 8,
-    prices the epilogues); interleaved rounds."""
+    builds and their no-epilogue builds (diag ABL 8, prices the epilogues); interleaved rounds."""
     M, D, H = M_TOK, 768, 12
     x = (torch.rand((M, D), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand((3 * D, D), generator=g, device=dev) * 2 - 1) / D ** 0.5).to(torch.bfloat16)
@@ -189,28 +186,17 @@ def tattn(dev, g):
     c = torch.zeros(3 * D, device=dev)
     rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
     p = torch.empty(M // 16 * H * 256, device=dev, dtype=torch.bfloat16)
-    o = {0: torch.empty(M, D, device=dev, dtype=torch.bfloat16), 16: torch.empty(M, D, device=dev, dtype=torch.bfloat16)}
-    pp = {0: torch.empty_like(p), 16: torch.empty_like(p)}
+    o = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
     st = lambda: torch.cuda.current_stream().cuda_stream
     wv = w[2 * D:].contiguous()
     def qk(abl):
-        nat.call("vp_dev_gemm_tattn_abl", 0, abl, x.data_ptr(), w.data_ptr(), M, D, pp[abl].data_ptr(), b.data_ptr(),
+        nat.call("vp_dev_gemm_tattn_abl", 0, abl, x.data_ptr(), w.data_ptr(), M, D, p.data_ptr(), b.data_ptr(),
                  rs.data_ptr(), c.data_ptr(), None, H, 50.0, st())
     def vv(abl):
-        nat.call("vp_dev_gemm_tattn_abl", 1, abl, x.data_ptr(), wv.data_ptr(), M, D, o[abl].data_ptr(), b.data_ptr(),
-                 rs.data_ptr(), c.data_ptr(), pp[abl].data_ptr(), H, 50.0, st())
-    o[64] = torch.empty_like(o[0])
-    pp[64] = pp[0]
-    for a in (0, 16, 64):
-        if a != 64:
-            qk(a)
-        vv(a)
-    torch.cuda.synchronize()
-    print("tattn scalar == packed (bitwise): P", bool(torch.equal(pp[0], pp[16])), "O", bool(torch.equal(o[0], o[16])),
-          "| V pf2 == product:", bool(torch.equal(o[0], o[64])), flush=True)
-    pp[8], o[8] = torch.empty_like(p), torch.empty_like(o[0])  # (no-epilogue builds: nothing written)
-    fns = {"qk-packed": lambda: qk(0), "qk-scalar": lambda: qk(16), "qk-noepi": lambda: qk(8),
-           "v-packed": lambda: vv(0), "v-scalar": lambda: vv(16), "v-noepi": lambda: vv(8), "v-pf2": lambda: vv(64)}
+        nat.call("vp_dev_gemm_tattn_abl", 1, abl, x.data_ptr(), wv.data_ptr(), M, D, o.data_ptr(), b.data_ptr(),
+                 rs.data_ptr(), c.data_ptr(), p.data_ptr(), H, 50.0, st())
+    qk(0)
+    fns = {"qk": lambda: qk(0), "qk-noepi": lambda: qk(8), "v": lambda: vv(0), "v-noepi": lambda: vv(8)}
     res = {k: [] for k in fns}
     for _ in range(3):
         for k, f in fns.items():
@@ -218,38 +204,11 @@ def tattn(dev, g):
     print("tattn:", " | ".join(f"{k} {min(v)*1e3:7.1f} us" for k, v in res.items()), flush=True)
 
 
-def early(dev, g):
-    """post (EPI_RESID_BF16_ST) and ffn_layer2 (EPI_RESID_FFN_BF16_ST) at the bench shape: product build vs
-    the build that requests the epilogue's first residual rows in the tile's last h1 (diag ABL 32),
-    bitwise check (the residual is updated in place, so each run starts from the same x), interleaved."""
-    for name, N, K, epi in (("post", 768, 768, nat.EPI_RESID_BF16_ST), ("ffn2", 768, 3072, nat.EPI_RESID_FFN_BF16_ST)):
-        M = M_TOK
-        a, w, b = operands(M, N, K, g, dev)
-        x0 = torch.randn((M, N), generator=g, device=dev).to(torch.bfloat16)
-        part = {k: torch.empty((N // 128, M, 2), device=dev) for k in (0, 32)}
-        o = {k: x0.clone() for k in (0, 32)}
-        st = lambda: torch.cuda.current_stream().cuda_stream
-        run = lambda k: nat.call("vp_dev_gemm_resid_abl", epi, k, a.data_ptr(), w.data_ptr(), M, N, K, o[k].data_ptr(),
-                                 b.data_ptr(), part[k].data_ptr(), st())
-        for k in (0, 32):
-            run(k)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(o[0], o[32])) and bool(torch.equal(part[0], part[32]))
-        res = {k: [] for k in (0, 32)}
-        for _ in range(3):
-            for k in (0, 32):
-                res[k].append(timeit(lambda: run(k)))
-        flop = 2.0 * M * N * K
-        print(f"{name} early residual == product (bitwise): {same}: " + " | ".join(
-            f"abl{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
-        del a, x0, o, part
-
-
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn, "early": early}
+    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn}
     modes.get(mode, compare)(dev, g)
 
 

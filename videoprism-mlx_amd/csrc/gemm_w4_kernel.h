@@ -87,25 +87,16 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
-// accumulators stay live); 16 = the fused temporal epilogues' LN fold in scalar instead of packed fp32
-// (bitwise equal; packed fp32 VALU beside MFMAs is an anti-lever in MI355X_MICROARCH.md's price list);
-// 32 = the residual rows of the epilogue's first block requested in the tile's last h1 instead of at
-// the epilogue's start (bitwise equal); 64 = the fused V launch's P / row-statistics loads 2 (sequence,
-// head) steps ahead instead of one (bitwise equal).
+// accumulators stay live).
 
-// the LN fold of 4 accumulator values (r * a + (m * c + b)), in packed pairs or (SCALAR, diag A/B
-// builds) one fp32 fma at a time -- the same two IEEE fmas per value either way, so bitwise equal
-template <bool SCALAR>
+// the LN fold of 4 accumulator values (r * a + (m * c + b)) in packed pairs: two IEEE fmas per value
+// (the scalar form is bitwise equal and measured no faster beside the fused epilogues' MFMAs:
+// QK launch 250.9 vs 246.5 us, V launch 161.8 vs 159.0)
 __device__ __forceinline__ void fold4(const f32x4& a, float r, float m, const float4& c, const float4& b, f32x2_t& lo,
                                       f32x2_t& hi) {
-  if constexpr (SCALAR) {
-    lo = f32x2_t{fmaf(r, a[0], fmaf(m, c.x, b.x)), fmaf(r, a[1], fmaf(m, c.y, b.y))};
-    hi = f32x2_t{fmaf(r, a[2], fmaf(m, c.z, b.z)), fmaf(r, a[3], fmaf(m, c.w, b.w))};
-  } else {
-    const f32x2_t rr = f32x2_t(r), mm = f32x2_t(m);
-    lo = __builtin_elementwise_fma(rr, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(mm, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
-    hi = __builtin_elementwise_fma(rr, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(mm, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
-  }
+  const f32x2_t rr = f32x2_t(r), mm = f32x2_t(m);
+  lo = __builtin_elementwise_fma(rr, f32x2_t{a[0], a[1]}, __builtin_elementwise_fma(mm, f32x2_t{c.x, c.y}, f32x2_t{b.x, b.y}));
+  hi = __builtin_elementwise_fma(rr, f32x2_t{a[2], a[3]}, __builtin_elementwise_fma(mm, f32x2_t{c.z, c.w}, f32x2_t{b.z, b.w}));
 }
 
 template <int EPI, bool NOPAD, bool S3, int ABL = 0, bool AVID = false>
@@ -290,22 +281,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     sched_fence();
   };
-  // the epilogue's residual / position rows of block (mt, nh, pass) -> ex[buffer][nh][pass], for the
-  // tile whose wave origin is (m0, n0)
-  const int er = lane >> 3, es = lane & 7;  // epilogue read-back: row pass*8 + er, column segment es
-  F8 ex[2][2][2];
-  int ex_m0 = 0, ex_n0 = 0;  // ABL 32: the current tile's wave origin (set at tile start)
-  auto fetch = [&](int bsel, int mt, int m0, int n0) {
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass)
-        ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
-  };
   // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
-  // 16 loads of K-tile g+2 into buffer cb.  last: the tile's last K-tile (ABL 32: block 0's residual
-  // rows are requested there, ahead of the next tile's W pieces)
-  auto h1 = [&](int cb, bool last) {
+  // 16 loads of K-tile g+2 into buffer cb
+  auto h1 = [&](int cb) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // S3: K-tile g+1 has landed once all but this K-tile's h0 A pieces (of g+2) are done
     if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -316,10 +294,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     sched_fence();
     __builtin_amdgcn_s_barrier();
     sched_fence();
-    if constexpr ((ABL & 32) != 0 && EpiTraits<EPI>::kExtra) {
-      if (last) fetch(0, 0, ex_m0, ex_n0);
-      sched_fence();
-    }
     const int an = a3 == 2 ? 0 : a3 + 1;  // S3: A buffer of K-tile g+1
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -350,6 +324,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   };
 
   int g = 0;
+  const int er = lane >> 3, es = lane & 7;  // epilogue read-back: row pass*8 + er, column segment es
   for (int j = 0; j < count; ++j) {
     // this tile's bias columns, requested before any of the tile's K-stream loads: vmcnt
     // retires in issue order, so a bias load issued in the epilogue would wait for the next
@@ -360,10 +335,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     {
       int ttm, ttn;
       coords(first + j * stride, ttm, ttn);
-      if constexpr ((ABL & 32) != 0) {
-        ex_m0 = ttm * BM + wm * 128;
-        ex_n0 = ttn * BN + wn * 128;
-      }
       const int nb = ttn * BN + wn * 128 + es * 8;
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) {
@@ -385,11 +356,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       }
     }
     h0(g & 1, true);
-    h1(g & 1, nk == 1);
+    h1(g & 1);
     ++g;
     for (int kt = 1; kt < nk; ++kt, ++g) {
       h0(g & 1, false);
-      h1(g & 1, kt == nk - 1);
+      h1(g & 1);
     }
 
     // ---- epilogue of tile j.  acc[nt][mt] holds D[row mb + 16*mt][cols nb + 16*nt + 4*(lane>>4)
@@ -466,7 +437,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                   f32x2_t lo, hi;
-                  fold4<(ABL & 16) != 0>(acc[hh * 4 + 2 * kk + i][mt], rsA[ml].x, rsA[ml].y, cc[2 * hh + i],
+                  fold4(acc[hh * 4 + 2 * kk + i][mt], rsA[ml].x, rsA[ml].y, cc[2 * hh + i],
                                          bb[2 * hh + i], lo, hi);
                   u[2 * i] = pack_bf16x2(lo.x, lo.y);
                   u[2 * i + 1] = pack_bf16x2(hi.x, hi.y);
@@ -533,26 +504,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           return *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + nh * 64) >> 6)) * 256 + lid * 4);
         };
         auto ld_rs = [&](int mt) { return *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + mt * 16 + r16)); };
-        // (ABL 64: kVpf = 2 (sequence, head) steps ahead instead of one)
-        constexpr int kVpf = (ABL & 64) ? 2 : 1;
-        bf16x4 pbq[kVpf];
-        float2 rsq[kVpf];
-#pragma unroll
-        for (int st = 0; st < kVpf; ++st) {
-          pbq[st] = ld_p(st & 7, st >> 3);
-          rsq[st] = ld_rs(st & 7);
-        }
+        bf16x4 pb_n = ld_p(0, 0);
+        float2 rs_n = ld_rs(0);
 #pragma unroll
         for (int nh = 0; nh < 2; ++nh) {
 #pragma unroll
           for (int mt = 0; mt < 8; ++mt) {
             char* vb = scr + (mt & 1) * 2048;  // double-buffered V block (16 rows x 64 bf16)
-            const int st = nh * 8 + mt, sl = st % kVpf;
-            const bf16x4 pb = pbq[sl];
-            const float r = rsq[sl].x, m = rsq[sl].y;
-            if (st + kVpf < 16) {
-              pbq[sl] = ld_p((st + kVpf) & 7, (st + kVpf) >> 3);
-              rsq[sl] = ld_rs((st + kVpf) & 7);
+            const bf16x4 pb = pb_n;
+            const float r = rs_n.x, m = rs_n.y;
+            if (mt < 7 || nh == 0) {
+              pb_n = ld_p((mt + 1) & 7, nh + (mt == 7));
+              rs_n = ld_rs((mt + 1) & 7);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -560,7 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
               const float4 c = *reinterpret_cast<const float4*>(lc + cofs);
               const float4 b = *reinterpret_cast<const float4*>(lc + 512 + cofs);
               f32x2_t lo, hi;
-              fold4<(ABL & 16) != 0>(acc[nh * 4 + q][mt], r, m, c, b, lo, hi);
+              fold4(acc[nh * 4 + q][mt], r, m, c, b, lo, hi);
               *reinterpret_cast<uint2*>(vb + vunit(r16, 4 * q + g4)) =
                   make_uint2(pack_bf16x2(lo.x, lo.y), pack_bf16x2(hi.x, hi.y));
             }
@@ -578,6 +541,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)
+    F8 ex[2][2][2];  // [buffer][nh][pass]
+    auto fetch = [&](int bsel, int mt) {
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass)
+          ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+    };
     // block G = (mt, nh): acc[nh*4 + q][mt], q = 0..3 -> scratch buffer G & 1.  Block G+1 is
     // written before block G is read back, so the LDS round trip overlaps the math and stores.
     auto put = [&](int G) {
@@ -593,14 +564,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     // es keeps the partials of mt == es, so the wave stores its 128 rows with 2 instructions
     float sv[2][8];
     float pS[2] = {0.f, 0.f}, pQ[2] = {0.f, 0.f};
-    if constexpr (Tr::kExtra && !(ABL & 32)) fetch(0, 0, m0, n0);
+    if constexpr (Tr::kExtra) fetch(0, 0);
     put(0);
 #pragma unroll
     for (int G = 0; G < 16; ++G) {
       const int mt = G >> 1, nh = G & 1;
       if (G + 1 < 16) put(G + 1);
       if constexpr (Tr::kExtra) {
-        if (nh == 0 && mt < 7) fetch((mt + 1) & 1, mt + 1, m0, n0);
+        if (nh == 0 && mt < 7) fetch((mt + 1) & 1, mt + 1);
       }
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
