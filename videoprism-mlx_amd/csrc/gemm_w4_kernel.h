@@ -31,6 +31,7 @@
 //    its M-blocks once per group of N-tiles (w4_ngrp), so a group's W stays L2-resident.
 #pragma once
 #include <cstdlib>
+#include <type_traits>
 
 #include "gemm_epilogue.h"
 
@@ -282,8 +283,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     sched_fence();
   };
   // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
-  // 16 loads of K-tile g+2 into buffer cb
-  auto h1 = [&](int cb) {
+  // 16 loads of K-tile g+2 into buffer cb.  DEFER (the fused V launch's last K-tile of a tile): the
+  // reads of set 0 are left to the end of the epilogue, so their 64 registers are free in it
+  auto h1 = [&](int cb, auto DEFER) {
+    constexpr bool defer = decltype(DEFER)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // S3: K-tile g+1 has landed once all but this K-tile's h0 A pieces (of g+2) are done
     if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const int an = a3 == 2 ? 0 : a3 + 1;  // S3: A buffer of K-tile g+1
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      rd(0, S3 ? an : (cb ^ 1), cb ^ 1, q);
+      if constexpr (!defer) rd(0, S3 ? an : (cb ^ 1), cb ^ 1, q);
       if constexpr (S3) {
         if (q >= 8) stage_piece(cb, q);  // W of K-tile g+2 into W buffer cb
       } else if constexpr (!(ABL & 4)) {
@@ -355,12 +358,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
             rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
-    h0(g & 1, true);
-    h1(g & 1);
-    ++g;
-    for (int kt = 1; kt < nk; ++kt, ++g) {
+    if constexpr (EpiTraits<EPI>::kVAttn) {  // the last K-tile peeled (K >= 2 BK, checked by the host)
+      h0(g & 1, true);
+      h1(g & 1, std::false_type{});
+      ++g;
+      for (int kt = 1; kt < nk - 1; ++kt, ++g) {
+        h0(g & 1, false);
+        h1(g & 1, std::false_type{});
+      }
       h0(g & 1, false);
-      h1(g & 1);
+      h1(g & 1, std::true_type{});
+      ++g;
+    } else {
+      h0(g & 1, true);
+      h1(g & 1, std::false_type{});
+      ++g;
+      for (int kt = 1; kt < nk; ++kt, ++g) {
+        h0(g & 1, false);
+        h1(g & 1, std::false_type{});
+      }
     }
 
     // ---- epilogue of tile j.  acc[nt][mt] holds D[row mb + 16*mt][cols nb + 16*nt + 4*(lane>>4)
@@ -487,55 +503,65 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         const int trq = r16 >> 2, trp = r16 & 3;
         auto vunit = [](int row, int u) { return row * 128 + ((u ^ (((row >> 1) & 3) << 2)) << 3); };
         // the LN-fold constants of the wave's 128 columns go to LDS once (c at +4 KiB, b' at +4.5 KiB
-        // of the wave's scratch) and are read where needed: held in registers for both heads they
-        // spilled the accumulator-layout fold
+        // of the wave's scratch) and are read into registers per head
         char* lc = scr + 4096;
         {
           const float* src = (lid < 32 ? ep.ln_c : ep.bias) + n0 + 4 * (lid & 31);
           *reinterpret_cast<float4*>(lc + (lid < 32 ? 0 : 512) + 16 * (lid & 31)) =
               *reinterpret_cast<const float4*>(src);
         }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the constants are in LDS
-        __builtin_amdgcn_wave_barrier();
-        // P^T fragment of (sequence mt, head nh) and (rstd, -mean*rstd) of row mt*16 + r16, one
-        // (sequence, head) ahead of their use
-        auto ld_p = [&](int mt, int nh) {
-          const int64_t sq = (int64_t)(m0 + mt * 16) >> 4;
-          return *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + nh * 64) >> 6)) * 256 + lid * 4);
+        // P^T fragment of (sequence mt, head nh), two (sequence, head) steps ahead of its use, and
+        // (rstd, -mean*rstd) of rows mt*16 + r16 (both heads)
+        auto ld_p = [&](int st) {
+          const int64_t sq = (int64_t)(m0 + (st & 7) * 16) >> 4;
+          return *reinterpret_cast<const bf16x4*>(pin + (sq * ep.heads + ((n0 + (st >> 3) * 64) >> 6)) * 256 + lid * 4);
         };
-        auto ld_rs = [&](int mt) { return *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + mt * 16 + r16)); };
-        bf16x4 pb_n = ld_p(0, 0);
-        float2 rs_n = ld_rs(0);
+        float2 rsv[8];
 #pragma unroll
-        for (int nh = 0; nh < 2; ++nh) {
+        for (int mt = 0; mt < 8; ++mt) rsv[mt] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + mt * 16 + r16));
+        bf16x4 pbq[2] = {ld_p(0), ld_p(1)};
+        float4 cc[4], bb[4];
+        auto ld_consts = [&](int nh) {
 #pragma unroll
-          for (int mt = 0; mt < 8; ++mt) {
-            char* vb = scr + (mt & 1) * 2048;  // double-buffered V block (16 rows x 64 bf16)
-            const bf16x4 pb = pb_n;
-            const float r = rs_n.x, m = rs_n.y;
-            if (mt < 7 || nh == 0) {
-              pb_n = ld_p((mt + 1) & 7, nh + (mt == 7));
-              rs_n = ld_rs((mt + 1) & 7);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int cofs = 4 * (nh * 64 + 16 * q + 4 * g4);
-              const float4 c = *reinterpret_cast<const float4*>(lc + cofs);
-              const float4 b = *reinterpret_cast<const float4*>(lc + 512 + cofs);
-              f32x2_t lo, hi;
-              fold4(acc[nh * 4 + q][mt], r, m, c, b, lo, hi);
-              *reinterpret_cast<uint2*>(vb + vunit(r16, 4 * q + g4)) =
-                  make_uint2(pack_bf16x2(lo.x, lo.y), pack_bf16x2(hi.x, hi.y));
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-              const bf16x4 vf = w4_tr_read(vb + vunit(4 * g4 + trq, 4 * dt + trp));
-              acc[nh * 4 + dt][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf, pb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // one sequence's accumulator reads at a time
+          for (int q = 0; q < 4; ++q) {
+            const int cofs = 4 * (nh * 64 + 16 * q + 4 * g4);
+            cc[q] = *reinterpret_cast<const float4*>(lc + cofs);
+            bb[q] = *reinterpret_cast<const float4*>(lc + 512 + cofs);
           }
+        };
+        // step st = (head st >> 3, sequence st & 7): v LN-folded, rounded and written to V block st & 1
+        auto fold_write = [&](int st) {
+          const int nh = st >> 3, mt = st & 7;
+          char* vb = scr + (st & 1) * 2048;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f32x2_t lo, hi;
+            fold4(acc[nh * 4 + q][mt], rsv[mt].x, rsv[mt].y, cc[q], bb[q], lo, hi);
+            *reinterpret_cast<uint2*>(vb + vunit(r16, 4 * q + g4)) = make_uint2(pack_bf16x2(lo.x, lo.y), pack_bf16x2(hi.x, hi.y));
+          }
+        };
+        // software-pipelined over the 16 steps: the transposed reads of step st are issued, then step
+        // st+1's block is folded and written (LDS executes one wave's operations in order, so no wait
+        // separates a block's writes from its reads), then step st's MFMAs wait for their reads only
+        ld_consts(0);
+        fold_write(0);
+#pragma unroll
+        for (int st = 0; st < 16; ++st) {
+          const int nh = st >> 3, mt = st & 7;
+          const char* vb = scr + (st & 1) * 2048;
+          bf16x4 vf[4];
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) vf[dt] = w4_tr_read(vb + vunit(4 * g4 + trq, 4 * dt + trp));
+          if (st + 1 < 16) {
+            if (st + 1 == 8) ld_consts(1);
+            fold_write(st + 1);
+          }
+          const bf16x4 pb = pbq[st & 1];
+          if (st + 2 < 16) pbq[st & 1] = ld_p(st + 2);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt)
+            acc[nh * 4 + dt][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[dt], pb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
@@ -639,6 +665,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       float* dst = ep.st_part + 2 * ((int64_t)p * ep.st_rows + m0 + es * 16 + er);
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) *reinterpret_cast<float2*>(dst + 16 * pass) = make_float2(pS[pass], pQ[pass]);
+    }
+    if constexpr (EpiTraits<EPI>::kVAttn) {  // the next tile's first fragments, deferred by its last h1
+      // (also after the last tile, where they are not used: a conditional read would keep the
+      // K-loop's stale set-0 registers live through the epilogue on the other path)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rd(0, a3, g & 1, q);
     }
   }
   // drain the tail's (clamped) loads before the workgroup's LDS is released
