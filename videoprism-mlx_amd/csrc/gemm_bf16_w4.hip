@@ -58,8 +58,13 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
     case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RELU_BF16: return launch_w4<EPI_RELU_BF16, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     // temporal layers' q|k|v projection with the attention fused (T = 16): S3 as the q|k|v GEMM
-    case EPI_QK_TATTN_LN: return launch_w4<EPI_QK_TATTN_LN, false, S3>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_V_TATTN_LN: return launch_w4<EPI_V_TATTN_LN, false, S3>(A, lda, W, ldw, M, N, K, ep, s);
+    // (their last K-tile is peeled: K >= 2 BK)
+    case EPI_QK_TATTN_LN:
+      if (K < 2 * BK) return hipErrorInvalidValue;
+      return launch_w4<EPI_QK_TATTN_LN, false, S3>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_V_TATTN_LN:
+      if (K < 2 * BK) return hipErrorInvalidValue;
+      return launch_w4<EPI_V_TATTN_LN, false, S3>(A, lda, W, ldw, M, N, K, ep, s);
   }
   return hipErrorInvalidValue;
 }

@@ -78,13 +78,13 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // pieces over both phases is.)
 // AVID: A is the video itself (patch embedding without a patch tensor): bf16 frames
 // [frames][16P][16P][3] of a 16x16 patch grid, so a 256-row tile is one frame and a piece's 8 rows
-// are 8 horizontally adjacent patches.  A patch's pixel row py is 3P contiguous channels-last values;
-// it is read as cpr = ceil(3P / 8) 16-B chunks at value offsets min(8 cr, 3P - 8) (the last chunk
-// overlaps its predecessor instead of running past the row segment), and chunk c = cpr py + cr of the
-// patch fills K columns 8c .. 8c + 7, so K = 64 ceil(P cpr / 8) (P = 18: 126 chunks, K = 1024).  W is
-// zero at the overlap and past the P cpr chunks, whose slots re-read chunk 0.  Each lane's source
-// offset thus depends on the K-tile (video_chunk_off below, a few VALU per K-tile).  lda = the
-// pixel-row length in elements (48 P); the buffer descriptor spans the M / 256 frames.
+// are 8 horizontally adjacent patches -- their pixel-row segments are contiguous in the frame, so a
+// piece instruction reads one 8 x 6P-byte run.  K-tile kt is patch pixel row kt (K = 64 P): its 3P
+// channels-last values are read as 16-B chunks at value offsets 0, 8, .., and min(8 j, 3P - 8) for the
+// row's last chunk j = cpr - 1 (cpr = ceil(3P / 8); it overlaps its predecessor instead of running
+// into the next patch), chunk slots j >= cpr re-read chunk 0; W is zero at the overlap and in those
+// slots, so no read leaves the patch's row segment.  The lane offsets are K-tile independent.  lda =
+// the pixel-row length in elements (48 P); the buffer descriptor spans the M / 256 frames.
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
@@ -151,11 +151,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // Lane: row (lane>>3) of the piece, LDS chunk (lane&7) <- source chunk (lane&7)^swz(row);
   // swz(row) of piece i depends only on i & 1.
   const uint32_t a_rb = (uint32_t)(lda * 2), w_rb = (uint32_t)(ldw * 2);
-  // AVID: a_rb = one pixel row of a frame (48 P values), 16 P pixel rows per frame; cpr chunks per
-  // patch pixel row, c / cpr = (c * av_mag) >> 16 for the chunk indices of a patch (< 1024 / cpr)
-  const int av_p = AVID ? (int)(lda / 48) : 0;
+  // AVID: a_rb = one pixel row of a frame (48 P values), 16 P pixel rows per frame, K-tile = one
+  // patch pixel row of 3P values in cpr 16-B chunks
+  const int av_p = AVID ? K / BK : 0;
   const int av_cpr = AVID ? (3 * av_p + 7) >> 3 : 1;
-  const uint32_t av_mag = AVID ? (65535u + (uint32_t)av_cpr) / (uint32_t)av_cpr : 0;
   const uint32_t prow_b = AVID ? (uint32_t)(6 * av_p) : 0;    // bytes of one patch's pixel row
   const uint32_t frame_b = AVID ? (uint32_t)(16 * av_p) * a_rb : 0;
   const uint64_t a_bytes = AVID ? (uint64_t)(M / BM) * frame_b : (uint64_t)M * a_rb;
@@ -165,16 +164,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   const int prow = lane >> 3;
   const uint32_t cE = (uint32_t)((lane & 7) ^ swz(prow)) * 16;       // even pieces
   const uint32_t cO = (uint32_t)((lane & 7) ^ swz(prow + 8)) * 16;   // odd pieces
-  const uint32_t vA[2] = {prow * (AVID ? prow_b : a_rb) + cE, prow * (AVID ? prow_b : a_rb) + cO};
-  // AVID: this lane's source offset in K-tile kt for even (par 0) / odd pieces: logical chunk
-  // (lane & 7) ^ swz of the K-tile row = patch chunk c = 8 kt + j
-  auto video_chunk_off = [&](int kt, int par) -> uint32_t {
-    const int c = kt * 8 + ((lane & 7) ^ swz(prow + 8 * par));
-    int py = (int)(((uint32_t)c * av_mag) >> 16);
-    int vo = min(8 * (c - py * av_cpr), 3 * av_p - 8);
-    if (c >= av_p * av_cpr) py = vo = 0;
-    return prow * prow_b + (uint32_t)py * a_rb + (uint32_t)vo * 2;
+  // AVID: logical chunk j = (lane & 7) ^ swz of a K-tile row -> value offset within the patch row
+  auto video_off = [&](int par) -> uint32_t {
+    const int jj = (lane & 7) ^ swz(prow + 8 * par);
+    const int vo = jj >= av_cpr ? 0 : min(8 * jj, 3 * av_p - 8);
+    return prow * prow_b + (uint32_t)vo * 2;
   };
+  const uint32_t vA[2] = {AVID ? video_off(0) : prow * a_rb + cE, AVID ? video_off(1) : prow * a_rb + cO};
   const uint32_t vW[2] = {prow * w_rb + cE, prow * w_rb + cO};
   typedef __attribute__((address_space(3))) void lds_void;
   // load stream: K-tile ld_g -> (tile ld_tm/ld_tn, K-tile ld_kt); the tail re-loads the last
@@ -200,15 +196,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     char* dst = (p >= 8 ? w_buf(buf) : a_buf(buf)) + (w * 8 + i) * 1024;
     if (p < 8) {
       uint32_t so;
-      uint32_t vo = vA[i & 1];
       if constexpr (AVID) {  // piece w*8+i: patch-grid row (w*8+i) >> 1, patches 8 ((w*8+i) & 1) + 0..7
         const int pc = w * 8 + i;
-        so = (uint32_t)ld_tm * frame_b + (uint32_t)((pc >> 1) * av_p) * a_rb + (uint32_t)(pc & 1) * 8 * prow_b;
-        vo = video_chunk_off(ld_kt, i & 1);
+        so = (uint32_t)ld_tm * frame_b + (uint32_t)((pc >> 1) * av_p + ld_kt) * a_rb + (uint32_t)(pc & 1) * 8 * prow_b;
       } else {
         so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vo, so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
     } else {
       const uint32_t so = (uint32_t)(ld_tn * BN + (w * 8 + i) * 8) * w_rb + ld_kt * (BK * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void*)dst, 16, vW[i & 1], so, 0, 0);
@@ -283,8 +277,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     sched_fence();
   };
   // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
-  // 16 loads of K-tile g+2 into buffer cb.  DEFER (the fused V launch's last K-tile of a tile): the
-  // reads of set 0 are left to the end of the epilogue, so their 64 registers are free in it
+  // 16 loads of K-tile g+2 into buffer cb.  DEFER (the fused temporal launches' last K-tile of a
+  // tile): the reads of set 0 are left to the end of the epilogue, so their 64 registers are free in it
   auto h1 = [&](int cb, auto DEFER) {
     constexpr bool defer = decltype(DEFER)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -358,7 +352,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
             rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
-    if constexpr (EpiTraits<EPI>::kVAttn) {  // the last K-tile peeled (K >= 2 BK, checked by the host)
+    if constexpr (EpiTraits<EPI>::kVAttn || EpiTraits<EPI>::kQkAttn) {  // last K-tile peeled (K >= 2 BK)
       h0(g & 1, true);
       h1(g & 1, std::false_type{});
       ++g;
@@ -428,22 +422,31 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         const float c1 = ep.cap_c1, c2 = ep.cap_c2;
         const int head = n0 >> 7;
         const uint32_t lane_off = (uint32_t)lid * 8u;  // this lane's 8 B of a 512-B P block
+        // the LN-fold constants of the wave's 128 columns go to LDS once (c at +0, b' at +512 of the
+        // wave's scratch) and are read per k-half from there (global reads per k-half waited behind
+        // the next tile's staging loads); the row statistics of all 8 sequences are read up front
+        char* lc = scr;
+        {
+          const float* src = (lid < 32 ? ep.ln_c : ep.bias) + n0 + 4 * (lid & 31);
+          *reinterpret_cast<float4*>(lc + (lid < 32 ? 0 : 512) + 16 * (lid & 31)) =
+              *reinterpret_cast<const float4*>(src);
+        }
+        float2 rsA[8];  // (rstd, -mean*rstd) of rows mt*16 + (lane & 15)
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+          rsA[mt] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + mt * 16 + (lane & 15)));
 #pragma unroll
         for (int mh = 0; mh < 2; ++mh) {
           float4 cc[4], bb[4];
-          float2 rsA[4];  // (rstd, -mean*rstd) of rows (mh*4 + ml)*16 + (lane & 15)
-#pragma unroll
-          for (int ml = 0; ml < 4; ++ml)
-            rsA[ml] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(m0 + (mh * 4 + ml) * 16 + (lane & 15)));
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh)  // cc/bb[2*hh + i]: block 2kk + i of q (hh = 0) / k (hh = 1)
 #pragma unroll
               for (int i = 0; i < 2; ++i) {
-                const int n = n0 + hh * 64 + 16 * (2 * kk + i) + 4 * g4;
-                cc[2 * hh + i] = *reinterpret_cast<const float4*>(ep.ln_c + n);
-                bb[2 * hh + i] = *reinterpret_cast<const float4*>(ep.bias + n);
+                const int cofs = 4 * (hh * 64 + 16 * (2 * kk + i) + 4 * g4);
+                cc[2 * hh + i] = *reinterpret_cast<const float4*>(lc + cofs);
+                bb[2 * hh + i] = *reinterpret_cast<const float4*>(lc + 512 + cofs);
               }
 #pragma unroll
             for (int ml = 0; ml < 4; ++ml) {
@@ -453,8 +456,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                   f32x2_t lo, hi;
-                  fold4(acc[hh * 4 + 2 * kk + i][mt], rsA[ml].x, rsA[ml].y, cc[2 * hh + i],
-                                         bb[2 * hh + i], lo, hi);
+                  fold4(acc[hh * 4 + 2 * kk + i][mt], rsA[mt].x, rsA[mt].y, cc[2 * hh + i], bb[2 * hh + i], lo, hi);
                   u[2 * i] = pack_bf16x2(lo.x, lo.y);
                   u[2 * i + 1] = pack_bf16x2(hi.x, hi.y);
                 }
@@ -487,6 +489,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
                 make_uint2(pack_bf16x2(p[0] * inv, p[1] * inv), pack_bf16x2(p[2] * inv, p[3] * inv));
           }
         }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) rd(0, a3, g & 1, q);  // the next tile's first fragments (deferred)
         continue;  // nothing else of this tile is stored
       } else {
         // O^T = V^T . P^T per (sequence mt, head nh) on 16x16x16 MFMAs: A = V^T by transposed

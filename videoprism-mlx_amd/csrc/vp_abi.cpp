@@ -125,7 +125,7 @@ int vp_finalize(vp_handle* h) {
           for (int64_t e = 0; e < 8; ++e) {
             const int64_t v = vo + e;
             if (cr == cpr - 1 && v < 8 * (cpr - 1)) continue;  // overlap with the row's previous chunk
-            for (int64_t n = 0; n < D; ++n) tv[(size_t)n * kv + 8 * (py * cpr + cr) + e] = k[(size_t)(py * 3 * P + v) * D + n];
+            for (int64_t n = 0; n < D; ++n) tv[(size_t)n * kv + 64 * py + 8 * cr + e] = k[(size_t)(py * 3 * P + v) * D + n];
           }
         }
       if ((rc = upload_mat(h, tv, &h->wpatch_v))) return rc;

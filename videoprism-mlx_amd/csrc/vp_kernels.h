@@ -84,12 +84,12 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
                         int N, int K, const EpiArgs& ep, hipStream_t s);
 // patch embedding straight from bf16 frames (no patch tensor): video [M/256 frames]
 // [16P][16P][3] (a 16x16 patch grid, so one 256-row tile is one frame), 3 <= P <= 21, epi
-// EPI_POS_BF16(_ST).  W [N][video_patch_k(P)]: patch pixel row py is read as cpr = ceil(3P/8) chunks
-// of 8 values at value offsets min(8 cr, 3P - 8); chunk c = cpr py + cr sits at columns 8c .. 8c+7,
-// W holding the patch-kernel row (py, vo + e) there except where the last chunk of a row overlaps its
-// predecessor (zero), and zeros past the P cpr chunks (video_patch_w packs it)
+// EPI_POS_BF16(_ST).  W [N][video_patch_k(P) = 64 P]: patch pixel row py is K-tile py, read as cpr =
+// ceil(3P/8) chunks of 8 values at value offsets min(8 j, 3P - 8) in slots j < cpr; W holds the
+// patch-kernel row (py, vo + e) at column 64 py + 8 j + e except where the last chunk overlaps its
+// predecessor and in the slots j >= cpr (zeros; video_patch_w packs it)
 inline int video_patch_cpr(int P) { return (3 * P + 7) / 8; }
-inline int video_patch_k(int P) { return (P * video_patch_cpr(P) + 7) / 8 * 64; }
+inline int video_patch_k(int P) { return 64 * P; }
 hipError_t gemm_bf16_w4_video(int epi, const bf16_t* video, int P, const bf16_t* W, int M, int N, const EpiArgs& ep,
                               hipStream_t s);
 // N-tile group size of the persistent tile order (gemm_bf16_w4.hip; shared by the diag kernels)

@@ -331,12 +331,12 @@ def dev_gemm_tattn(which, a, w, bias, ln_rs, ln_c, out, heads, cap, p=None, stre
 
 def video_patch_w(k, P):
     """The fused patch embedding's weight layout (vp_kernels.h video_patch_k; packed the same way by
-    vp_finalize): k [P*P*3, N] (the patch kernel) -> [N, K] with patch pixel row py read as
-    cpr = ceil(3P/8) chunks of 8 values at value offsets min(8 cr, 3P - 8), chunk c = cpr py + cr at
-    columns 8c..8c+7, zero where a row's last chunk overlaps its predecessor and past the P cpr chunks."""
+    vp_finalize): k [P*P*3, N] (the patch kernel) -> [N, 64 P]: patch pixel row py is K-tile py, read as
+    cpr = ceil(3P/8) chunks of 8 values at value offsets min(8 j, 3P - 8) in slots j < cpr (columns
+    64 py + 8 j ..); zero where a row's last chunk overlaps its predecessor and in the slots j >= cpr."""
     import torch
     cpr = (3 * P + 7) // 8
-    kv = (P * cpr + 7) // 8 * 64
+    kv = 64 * P
     out = torch.zeros(k.shape[1], kv, dtype=k.dtype)
     for py in range(P):
         for cr in range(cpr):
@@ -345,7 +345,7 @@ def video_patch_w(k, P):
                 v = vo + e
                 if cr == cpr - 1 and v < 8 * (cpr - 1):
                     continue
-                out[:, 8 * (py * cpr + cr) + e] = k[py * 3 * P + v]
+                out[:, 64 * py + 8 * cr + e] = k[py * 3 * P + v]
     return out
 
 
