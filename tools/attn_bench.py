@@ -65,33 +65,40 @@ def main():
 
 def long_variants():
     """The auxiliary (4096-token) attention at the LvT-Large bench shape (32 clips x 16 heads, S = 4096):
-    the product kernel (var 0) against its diag-library A/B builds (1: scalar polynomial numerator),
-    bitwise check, interleaved rounds.  VP_DIAG_LIB=1 python tools/attn_bench.py long"""
+    the product kernel (var 0) against its diag-library A/B builds (1: scalar polynomial numerator,
+    2: quadratic tier for tiles with |logit| <= 0.24 cap, 4: packed row sum; bits combine), at two
+    logit scales (std 0.5: every tile in the quadratic tier; std 6: mixed tiers), interleaved rounds.
+    VP_DIAG_LIB=1 python tools/attn_bench.py long"""
     dev = torch.device("cuda:0")
     nseq, heads, S = 32, 16, 4096
-    g = torch.Generator(device=dev).manual_seed(0)
     D = heads * 64
-    qkv = torch.randn((nseq * S, 3 * D), generator=g, device=dev)
-    qkv[:, :D] *= 0.125 * 0.5
-    qkv = qkv.to(torch.bfloat16)
     st = lambda: torch.cuda.current_stream().cuda_stream
-    outs = {}
-    fns = {}
-    for var in (0, 1):
-        outs[var] = torch.empty((nseq * S, D), device=dev, dtype=torch.bfloat16)
-        fns[f"var{var}"] = (lambda var=var: nat.call("vp_dev_attention_long_var", var, qkv.data_ptr(),
-                                                     outs[var].data_ptr(), nseq, S, heads, 50.0, st()))
-    for f in fns.values():
-        f()
-    torch.cuda.synchronize()
-    print("var1 == var0 (bitwise):", bool(torch.equal(outs[0], outs[1])), flush=True)
-    res = {k: [] for k in fns}
-    for _ in range(3):
-        for k, f in fns.items():
-            res[k].append(timeit(f, iters=5, warm=1))
-    flop = 4.0 * nseq * S * S * D
-    print("aux attention:", " ".join(f"{k}: {min(v):7.3f} ms ({flop/min(v)/1e9:5.0f} TF)" for k, v in res.items()),
-          flush=True)
+    variants = (0, 1, 2, 4, 6)
+    for qscale in (0.0625, 0.75):
+        g = torch.Generator(device=dev).manual_seed(0)
+        qkv = torch.randn((nseq * S, 3 * D), generator=g, device=dev)
+        qkv[:, :D] *= qscale
+        qkv = qkv.to(torch.bfloat16)
+        outs, fns = {}, {}
+        for var in variants:
+            outs[var] = torch.empty((nseq * S, D), device=dev, dtype=torch.bfloat16)
+            fns[f"var{var}"] = (lambda var=var: nat.call("vp_dev_attention_long_var", var, qkv.data_ptr(),
+                                                         outs[var].data_ptr(), nseq, S, heads, 50.0, st()))
+        for f in fns.values():
+            f()
+        torch.cuda.synchronize()
+        ref = outs[0].float()
+        print(f"logit std {qscale * 8:.1f}: " + " ".join(
+            f"var{v} vs var0 max {(outs[v].float() - ref).abs().max().item():.2e} (bitwise {bool(torch.equal(outs[v], outs[0]))})"
+            for v in variants[1:]), flush=True)
+        res = {k: [] for k in fns}
+        for _ in range(3):
+            for k, f in fns.items():
+                res[k].append(timeit(f, iters=5, warm=1))
+        flop = 4.0 * nseq * S * S * D
+        print("aux attention:", " ".join(f"{k}: {min(v):7.3f} ms ({flop/min(v)/1e9:5.0f} TF)" for k, v in res.items()),
+              flush=True)
+        del qkv, outs
 
 
 if __name__ == "__main__":

@@ -1,6 +1,7 @@
 // A/B builds of the auxiliary (4096-token) attention kernel (videoprism-mlx_amd/csrc/
 // attention_long_kernel.h) for the tools' diag library: var 0 = the product kernel, 1 = the
-// polynomial numerator in scalar instead of packed fp32 (bitwise the same output).
+// polynomial numerator in scalar instead of packed fp32 (bitwise the same output), 2 = quadratic tier
+// for small logits, 4 = packed row sum (bits combine: 6, 7).
 #include "attention_long_kernel.h"
 
 extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int64_t num_seq, int64_t S,
@@ -10,5 +11,9 @@ extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int6
   hipError_t e = hipErrorInvalidValue;
   if (var == 0) e = launch_attn_long<0>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 1) e = launch_attn_long<1>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 2) e = launch_attn_long<2>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 4) e = launch_attn_long<4>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 6) e = launch_attn_long<6>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 7) e = launch_attn_long<7>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   return e == hipSuccess ? 0 : -1;
 }

@@ -28,7 +28,9 @@ constexpr int kLgStageBytes = 2 * kLgChunk * 128;  // K then V, 128 B per key ro
 constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 
 // VAR (A/B builds of the diag library; the product uses 0): 1 = the polynomial numerator in scalar
-// instead of packed fp32 arithmetic (bitwise the same values: one IEEE fma per step either way)
+// instead of packed fp32 arithmetic (bitwise the same values: one IEEE fma per step either way);
+// 2 = the quadratic tier for tiles with |x| <= 0.24 cap (vp_common.h capped_exp16 QUAD); 4 = the row
+// sum accumulated in packed pairs
 template <int VAR = 0>
 __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* __restrict__ qkv,
                                                                   bf16_t* __restrict__ o, int S,
@@ -86,6 +88,8 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
   const float c2 = cap * kLog2e;
   f32x16 y0 = {}, y1 = {};
   float lsum = 0.0f;
+  typedef float f2_t __attribute__((ext_vector_type(2)));
+  f2_t lsum2 = {0.0f, 0.0f};
   const int krow_l = lane & 31;
   const int g = lane >> 4;
   const int li = lane & 15;
@@ -123,9 +127,14 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
-      capped_exp16<(VAR & 1) == 0>(x, p, c1, c2, cp);
+      capped_exp16<(VAR & 1) == 0, (VAR & 2) != 0>(x, p, c1, c2, cp);
+      if constexpr ((VAR & 4) != 0) {  // row sum in packed pairs
 #pragma unroll
-      for (int i = 0; i < 16; ++i) lsum += p[i];
+        for (int i = 0; i < 16; i += 2) lsum2 += f2_t{p[i], p[i + 1]};
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lsum += p[i];
+      }
       bf16x8 pf[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -160,6 +169,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
       }
     }
   }
+  if constexpr ((VAR & 4) != 0) lsum = lsum2.x + lsum2.y;
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;
   bf16_t* op = o + ((int64_t)seq * S + q0 + (lane & 31)) * D + h * 64 + 4 * half;

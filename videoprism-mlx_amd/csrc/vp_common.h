@@ -69,26 +69,38 @@ __device__ __forceinline__ float capped_exp_exact(float x, float two_log2e_over_
 // cubic (relative error 4.5e-7, tools/fit_gelu.py fit_tanh), so the numerator is
 // exp2(x * P(x^2)) with k_i = log2e t_i / cap^(2i) folded on the host (make_cap_poly); tiles
 // holding a larger logit take the exact path (wave-uniform branch).
+// QUAD tier (tiles whose logits all satisfy |x| <= 0.24 cap): T fitted by a quadratic on v in
+// [0, 0.24^2] (relative error 3.5e-7, tools/fit_gelu.py fit_tanh(0.24, 2)), coefficients q0..q2.
 struct CapPoly {
   float k0, k1, k2, k3, x0;
+  float q0, q1, q2, x1;
 };
 
 inline CapPoly make_cap_poly(float cap) {
   const double t[4] = {0.9999995827674866, -0.33327752351760864, 0.1321016252040863, -0.045063190162181854};
+  const double u[3] = {0.9999996877028773, -0.33323595618512314, 0.12879159575308177};
   const double l2e = 1.4426950408889634, c2 = (double)cap * cap;
   return CapPoly{(float)(l2e * t[0]), (float)(l2e * t[1] / c2), (float)(l2e * t[2] / (c2 * c2)),
-                 (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap};
+                 (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap,
+                 (float)(l2e * u[0]), (float)(l2e * u[1] / c2), (float)(l2e * u[2] / (c2 * c2)), 0.24f * cap};
 }
 
 // PACKED: the polynomial in pairs of packed fp32 (v_pk_mul_f32 / v_pk_fma_f32), else scalar fp32
 // (the same IEEE operations per value, so bitwise the same result; packed fp32 VALU beside another
 // wave's MFMAs is priced as an anti-lever in MI355X_MICROARCH.md's price list)
-template <bool PACKED = true>
+template <bool PACKED = true, bool QUAD = false>
 __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
   float mx = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
-  if (__builtin_amdgcn_ballot_w64(mx > cp.x0) == 0) {
+  if (QUAD && __builtin_amdgcn_ballot_w64(mx > cp.x1) == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float u = x[i] * x[i];
+      const float P = fmaf(fmaf(cp.q2, u, cp.q1), u, cp.q0);
+      p[i] = __builtin_amdgcn_exp2f(x[i] * P);
+    }
+  } else if (__builtin_amdgcn_ballot_w64(mx > cp.x0) == 0) {
     if constexpr (PACKED) {
       typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
