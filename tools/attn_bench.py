@@ -66,7 +66,8 @@ def main():
 def long_variants():
     """The auxiliary (4096-token) attention at the LvT-Large bench shape (32 clips x 16 heads, S = 4096):
     the product kernel (var 0) against its diag-library A/B builds (1: scalar polynomial numerator,
-    2: quadratic tier for tiles with |logit| <= 0.24 cap, 4: packed row sum; bits combine), at two
+    2: without the quadratic tier for tiles with |logit| <= 0.24 cap, 4: scalar row sum; 6 = round 3's
+    kernel), at two
     logit scales (std 0.5: every tile in the quadratic tier; std 6: mixed tiers), interleaved rounds.
     VP_DIAG_LIB=1 python tools/attn_bench.py long"""
     dev = torch.device("cuda:0")

@@ -1,7 +1,8 @@
 // A/B builds of the auxiliary (4096-token) attention kernel (videoprism-mlx_amd/csrc/
 // attention_long_kernel.h) for the tools' diag library: var 0 = the product kernel, 1 = the
-// polynomial numerator in scalar instead of packed fp32 (bitwise the same output), 2 = quadratic tier
-// for small logits, 4 = packed row sum (bits combine: 6, 7).
+// polynomial numerator in scalar instead of packed fp32 (bitwise the same output), 2 = without the
+// quadratic tier for small logits, 4 = the row sum one value at a time (bits combine: 6 = round 3's
+// kernel, 7).
 #include "attention_long_kernel.h"
 
 extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int64_t num_seq, int64_t S,

@@ -27,10 +27,12 @@ constexpr int kLgStages = 4;
 constexpr int kLgStageBytes = 2 * kLgChunk * 128;  // K then V, 128 B per key row
 constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 
-// VAR (A/B builds of the diag library; the product uses 0): 1 = the polynomial numerator in scalar
-// instead of packed fp32 arithmetic (bitwise the same values: one IEEE fma per step either way);
-// 2 = the quadratic tier for tiles with |x| <= 0.24 cap (vp_common.h capped_exp16 QUAD); 4 = the row
-// sum accumulated in packed pairs
+// The numerator takes the quadratic tier on tiles whose logits all satisfy |x| <= 0.24 cap (vp_common.h
+// capped_exp16 QUAD: as accurate as the cubic) and the row sum accumulates in packed pairs; with logits
+// of std 0.5 / 6 (tools/attn_bench.py long, LvT-Large shape) 2.606 / 2.926 ms vs 2.828 / 2.953 without
+// either.  VAR (A/B builds of the diag library; the product uses 0): 1 = the polynomial numerator in
+// scalar instead of packed fp32 arithmetic (bitwise the same values); 2 = no quadratic tier; 4 = the
+// row sum one value at a time
 template <int VAR = 0>
 __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* __restrict__ qkv,
                                                                   bf16_t* __restrict__ o, int S,
@@ -127,8 +129,8 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
-      capped_exp16<(VAR & 1) == 0, (VAR & 2) != 0>(x, p, c1, c2, cp);
-      if constexpr ((VAR & 4) != 0) {  // row sum in packed pairs
+      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0>(x, p, c1, c2, cp);
+      if constexpr ((VAR & 4) == 0) {  // row sum in packed pairs
 #pragma unroll
         for (int i = 0; i < 16; i += 2) lsum2 += f2_t{p[i], p[i + 1]};
       } else {
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
       }
     }
   }
-  if constexpr ((VAR & 4) != 0) lsum = lsum2.x + lsum2.y;
+  if constexpr ((VAR & 4) == 0) lsum = lsum2.x + lsum2.y;
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;
   bf16_t* op = o + ((int64_t)seq * S + q0 + (lane & 31)) * D + h * 64 + 4 * half;
