@@ -114,3 +114,15 @@ extern "C" void launch(float* o, const int* idx) { hipLaunchKernelGGL(spill_kern
     subprocess.run([HIPCC, *FLAGS, "-fPIC", "-shared", str(src), "-o", str(lib)], check=True, capture_output=True)
     bad = ck.resource_violations(str(lib))
     assert bad and "private_segment_fixed_size" in bad[0], bad
+
+
+def test_every_source_kernel_has_device_code(tmp_path):
+    """`make` also refuses a library that lacks the device code of any __global__ function its sources
+    define (a compile once dropped a whole translation unit's kernels silently, rc 0)."""
+    lib = _native.library_path()
+    srcs = _hip_sources()
+    assert ck.missing_kernels(lib, srcs) == []
+    extra = tmp_path / "extra.hip"
+    extra.write_text("__global__ __launch_bounds__(64) void not_built_kernel(float* o) { o[0] = 1.f; }\n")
+    assert ck.missing_kernels(lib, srcs + [str(extra)]) == ["not_built_kernel"]
+

@@ -121,6 +121,26 @@ def resource_violations(lib_path: str):
     return bad
 
 
+_GLOBAL_FN = re.compile(r"__global__\s+(?:__launch_bounds__\s*\([^)]*\)\s*)?void\s+(\w+)\s*\(")
+
+
+def missing_kernels(lib_path: str, sources):
+    """__global__ functions defined in `sources` of which the library holds no device code at all --
+    the failure of a host + device compile that silently dropped a translation unit's kernels (seen
+    once with a non-literal cache-policy argument to an LDS-DMA builtin: object built, rc 0, kernels
+    and their stubs gone, the library still linked)."""
+    have = set()
+    for k in kernels(lib_path):
+        m = re.match(r"_ZN2vp12_GLOBAL__N_1\d+(\w+?)(?:I|E|v|P)", k[".name"])
+        have.add(m.group(1) if m else k[".name"])
+    want = set()
+    for src in sources:
+        if src.endswith((".hip", ".h")) and os.path.exists(src):
+            want.update(_GLOBAL_FN.findall(open(src).read()))
+    names = " ".join(k[".name"] for k in kernels(lib_path))
+    return sorted(w for w in want if w not in have and w not in names)
+
+
 # ------------------------------------------------------------------------------------------------
 # inline-asm loads in the sources
 # ------------------------------------------------------------------------------------------------
@@ -294,6 +314,11 @@ def main(argv):
     cmd = argv[1]
     if cmd == "resources":
         bad = resource_violations(argv[2])
+        missing = missing_kernels(argv[2], argv[3:])
+        if missing:
+            print("check_kernels: no device code for kernels defined in the sources:\n  " + "\n  ".join(missing),
+                  file=sys.stderr)
+            return 1
         n = len(kernels(argv[2]))
         if bad:
             print("check_kernels: scratch / spills in product kernels:\n  " + "\n  ".join(bad), file=sys.stderr)

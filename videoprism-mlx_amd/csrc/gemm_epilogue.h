@@ -27,6 +27,12 @@ struct EpiTraits {
                                      EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST;
   static constexpr bool kPos = EPI == EPI_POS_F32 || EPI == EPI_POS_BF16 || EPI == EPI_POS_BF16_ST;
   static constexpr bool kExtra = kResidF32 || kResidBf16 || kPos;
+  // residual-stream producers (bf16 path): their A (the attention output / the FFN hidden activation)
+  // is read once, so it is staged with nontemporal loads, and the residual stream they write in place
+  // is stored with default-policy (cache-allocating) stores -- the next readers of the residual stream
+  // (the LN-folded consumer GEMM, the next residual epilogue) then find it in the Infinity Cache, which
+  // the once-read streams (q|k|v, attention output, hidden activation) no longer displace
+  static constexpr bool kResidStream = EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST;
   static constexpr bool kRelu = EPI == EPI_RELU_BF16;
   static constexpr bool kKeep = kGelu || kRelu || kResidF32 || kResidBf16;
   static constexpr bool kOutBf16 = !(EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN || EPI == EPI_POS_F32);

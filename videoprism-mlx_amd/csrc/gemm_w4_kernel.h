@@ -202,7 +202,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       } else {
         so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
+      if constexpr (EpiTraits<EPI>::kResidStream)  // aux 2: nt
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 2);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)dst, 16, vA[i & 1], so, 0, 0);
     } else {
       const uint32_t so = (uint32_t)(ld_tn * BN + (w * 8 + i) * 8) * w_rb + ld_kt * (BK * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void*)dst, 16, vW[i & 1], so, 0, 0);
@@ -634,7 +637,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
         }
         {
-          const epi_u32x4 pk = epi_store8<EPI, true, !NOPAD>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          const epi_u32x4 pk = epi_store8<EPI, !Tr::kResidStream, !NOPAD>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
           if constexpr (Tr::kStats) {
             float y[8];
 #pragma unroll
