@@ -53,9 +53,9 @@ constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 
 // q|k|v layout by strides (elements): row rs, head hs, section (q -> k -> v) sec; the row-major
 // fused projection output is (3D, 64, D).  O goes through LDS and leaves as whole 128-B row
-// segments (8 rows per store).  q|k|v are read and O written with nontemporal accesses (each is
-// touched once), so they do not displace the residual stream from the Infinity Cache (gemm_epilogue.h
-// kResidStream).
+// segments (8 rows per store); O is written with nontemporal stores (read once, by the post
+// projection), so it does not displace the residual stream from the Infinity Cache (gemm_epilogue.h
+// kResidStream).  (Nontemporal q|k|v loads measured slower: 2.45 vs 2.37-2.40 ms per step.)
 template <bool MASK>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
 #pragma unroll
     for (int kd = 0; kd < 4; ++kd)
-      asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(qf[kd]) : "v"(qp + 16 * kd));
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qp + 16 * kd));
   }
   // ---- stage K and V in 4 chunks of 64 keys, chunk-major: wave w loads K piece c*8+w and
   // V piece 32+c*8+w of chunk c (a piece = 8 keys x 128 B), so key tiles 2c, 2c+1 can start as
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       const int row = (piece & 31) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
       const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * sec : sec) + c * 8;
-      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 2);  // nt
+      __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
     }
   if constexpr (MASK) {  // (padded batches: no streaming)
     if (threadIdx.x < kSpS) kp[threadIdx.x] = key_pad[(int64_t)seq * kSpS + threadIdx.x];
