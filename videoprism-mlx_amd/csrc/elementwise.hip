@@ -242,37 +242,22 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 }
 
 // ---- LayerNorm statistics for the GEMM-folded LayerNorm (EPI_*_LN) ----
-// partials: st[p][row] = (sum, M2) over columns [128p, 128p+128) of the stored bf16 row.  PP: the
-// partial count as a compile-time constant (D = 768: 6, D = 1024: 8), so the P loads are all in flight
-// at once -- with a run-time count each iteration waited for its load (6 serial memory latencies:
-// 5.3 us per launch, 31 launches per Base step); PP = 0: run-time P
+// partials: st[p][row] = (sum, M2) over columns [128p, 128p+128) of the stored bf16 row
+// (vp_common.h ln_combine).  PP: the partial count as a compile-time constant (D = 768: 6, 1024: 8),
+// so the P loads are all in flight at once -- with a run-time count each iteration waited for its load
+// (6 serial memory latencies: 5.3 us per launch); PP = 0: run-time P <= 16
 template <int PP>
 __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __restrict__ st, int P_rt,
                                                                 int64_t M, float* __restrict__ rs_out) {
+  constexpr int PMAX = PP > 0 ? PP : 16;
   const int P = PP > 0 ? PP : P_rt;
   const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (row >= M) return;
-  float S[16], Q[16];
-  float tot = 0.f;
+  float2 pt[PMAX];
 #pragma unroll
-  for (int p = 0; p < (PP > 0 ? PP : 16); ++p) {
-    if (PP == 0 && p >= P) break;
-    const float2 v = *reinterpret_cast<const float2*>(st + 2 * ((int64_t)p * M + row));
-    S[p] = v.x;
-    Q[p] = v.y;
-    tot += v.x;
-  }
-  const float D = 128.0f * P;
-  const float mean = tot / D;
-  float m2 = 0.f;
-#pragma unroll
-  for (int p = 0; p < (PP > 0 ? PP : 16); ++p) {  // Chan: M2 = sum Q_p + n_p (mean_p - mean)^2
-    if (PP == 0 && p >= P) break;
-    const float d = S[p] * (1.0f / 128.0f) - mean;
-    m2 += Q[p] + 128.0f * d * d;
-  }
-  const float rs = 1.0f / sqrtf(m2 / D + 1e-6f);
-  *reinterpret_cast<float2*>(rs_out + 2 * row) = make_float2(rs, -mean * rs);
+  for (int p = 0; p < PMAX; ++p)
+    pt[p] = p < P ? *reinterpret_cast<const float2*>(st + 2 * ((int64_t)p * M + row)) : make_float2(0.f, 0.f);
+  *reinterpret_cast<float2*>(rs_out + 2 * row) = ln_combine(pt, P);
 }
 
 // two-pass statistics straight from bf16 rows, one wave per row

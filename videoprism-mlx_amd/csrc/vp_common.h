@@ -130,6 +130,29 @@ __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1
   }
 }
 
+// LayerNorm statistics of one row from P partials (sum S_p, sum of squares about the partial mean Q_p)
+// over 128 columns each (Chan): M2 = sum Q_p + 128 (S_p / 128 - mean)^2 -> (rstd, -mean * rstd),
+// eps 1e-6 (layers.py:225-243).  Shared by ln_stats_finalize and the GEMMs that combine the partials
+// themselves, so both give the same bits.
+template <int PMAX>
+__device__ __forceinline__ float2 ln_combine(const float2 (&pt)[PMAX], int P) {
+  float tot = 0.f;
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p)
+    if (p < P) tot += pt[p].x;
+  const float D = 128.0f * P;
+  const float mean = tot / D;
+  float m2 = 0.f;
+#pragma unroll
+  for (int p = 0; p < PMAX; ++p)
+    if (p < P) {
+      const float d = fmaf(pt[p].x, 1.0f / 128.0f, -mean);
+      m2 = m2 + fmaf(128.0f * d, d, pt[p].y);
+    }
+  const float rs = 1.0f / sqrtf(m2 / D + 1e-6f);
+  return make_float2(rs, -mean * rs);
+}
+
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---- LDS reads hipcc must not wait for with vmcnt (the attention kernels' K/V chunks land by
