@@ -364,38 +364,6 @@ def _ln_ref(x, gamma1p, beta):
 
 
 @pytest.mark.parametrize("epi", [nat.EPI_BF16_LN, nat.EPI_GELU_LN])
-@pytest.mark.parametrize("M,N,K", [(2048, 2304, 768), (1024, 3072, 768), (512, 1024, 1024)])
-def test_gemm_ln_fold_from_partials(cuda, epi, M, N, K):
-    """The LN-folded GEMM that combines the producers' partial row statistics itself (the forward's
-    spatial layers: no ln_stats_finalize launch between producer and consumer) is bitwise the GEMM fed
-    with ln_stats_finalize's (rstd, -mean*rstd) rows of the same partials -- both use ln_combine."""
-    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
-    x = _bf(torch.randn(M, K, generator=g) * 2 + 0.5)
-    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5)
-    b = torch.randn(N, generator=g) * 0.1
-    c = w.double().sum(1).float()
-    pad = (torch.rand(M, generator=g) < 0.2).float()
-    P = K // 128
-    blocks = x.double().reshape(M, P, 128)
-    mu = blocks.mean(2)
-    part = torch.stack([blocks.sum(2), ((blocks - mu[:, :, None]) ** 2).sum(2)], 2).permute(1, 0, 2)
-    part = part.float().contiguous().to(cuda)                      # [P][M][2]
-    rs = torch.empty(M, 2, device=cuda)
-    nat.dev_ln_stats(part, M, K, rs, from_partials=True)
-    rp = pad.to(cuda) if epi == nat.EPI_GELU_LN else None
-    o1 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    o2 = torch.empty_like(o1)
-    nat.dev_gemm_ln(x.to(cuda), w.to(cuda), b.to(cuda), epi, o1, ln_rs=rs, ln_c=c.to(cuda), rowpad=rp)
-    nat.dev_gemm_ln_part(x.to(cuda), w.to(cuda), b.to(cuda), epi, o2, part, c.to(cuda), rowpad=rp)
-    torch.cuda.synchronize()
-    assert torch.equal(o1, o2), (o1.float() - o2.float()).abs().max().item()
-    # and the finalised statistics are the fp64 LayerNorm statistics of x
-    xd = x.double()
-    rstd = 1 / torch.sqrt(xd.var(1, unbiased=False) + 1e-6)
-    assert torch.allclose(rs[:, 0].double().cpu(), rstd, rtol=2e-5)
-
-
-@pytest.mark.parametrize("epi", [nat.EPI_BF16_LN, nat.EPI_GELU_LN])
 @pytest.mark.parametrize("M,N,K", [(1024, 2304, 768), (512, 3072, 768), (256, 1024, 1024)])
 def test_gemm_ln_fold(cuda, epi, M, N, K):
     """LN(x).W + b computed as rstd*(x.W') - mean*rstd*c + b' with W' = W diag(gamma),

@@ -347,22 +347,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           cl[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64);
           ch[nh] = *reinterpret_cast<const float4*>(ep.ln_c + nb + nh * 64 + 4);
         }
-        if (ep.ln_p > 0) {  // the producers' partials of rows m0w + lane (slots 0..7) and m0w + 64 + lane (8..15)
-          const int64_t rb = (int64_t)ttm * BM + wm * 128 + lane;
+        const int mb = ttm * BM + wm * 128 + er;
 #pragma unroll
-          for (int sl = 0; sl < 16; ++sl) {
-            const int h = sl >> 3, p = sl & 7;
-            rs[sl >> 1][sl & 1] = p < ep.ln_p ? *reinterpret_cast<const float2*>(ep.ln_part + 2 * ((int64_t)p * ep.ln_rows + rb + 64 * h))
-                                              : make_float2(0.f, 0.f);
-          }
-        } else {
-          const int mb = ttm * BM + wm * 128 + er;
+        for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-          for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-            for (int pass = 0; pass < 2; ++pass)
-              rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
-        }
+          for (int pass = 0; pass < 2; ++pass)
+            rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
     if constexpr (EpiTraits<EPI>::kVAttn || EpiTraits<EPI>::kQkAttn) {  // last K-tile peeled (K >= 2 BK)
@@ -580,23 +570,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
             acc[nh * 4 + dt][mt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vf[dt], pb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
-      }
-    }
-    if constexpr (Tr::kLn) {
-      if (ep.ln_p > 0) {  // combine the two rows' partials, exchange through the wave's scratch
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float2 pt[8];
-#pragma unroll
-          for (int p = 0; p < 8; ++p) pt[p] = rs[(h * 8 + p) >> 1][p & 1];
-          *reinterpret_cast<float2*>(scr + (h * 64 + lane) * 8) = ln_combine(pt, ep.ln_p);
-        }
-        // (LDS executes one wave's operations in order: these reads see the writes above, and the
-        // block transpositions below overwrite the table only after them)
-#pragma unroll
-        for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-          for (int pass = 0; pass < 2; ++pass) rs[mt][pass] = *reinterpret_cast<const float2*>(scr + (mt * 16 + pass * 8 + er) * 8);
       }
     }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a

@@ -272,9 +272,8 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
     VP_HIP(expand_paddings(frame_paddings, (int)B, (int)T, Nsp, pad_btn, pad_bnt, s));
   }
   // bf16: LayerNorms inside the layers are folded into the consuming GEMMs (EPI_*_LN); the
-  // residual-stream producers emit partial row statistics (EPI_*_ST); the LN-folded GEMMs combine
-  // them (EpiArgs::ln_part), ln_stats_finalize turns them into (rstd, -mean*rstd) rows only for the
-  // fused temporal launches
+  // residual-stream producers emit row statistics (EPI_*_ST) that ln_stats_finalize turns into
+  // (rstd, -mean*rstd) per row
   Fwd f;
   f.s = s; f.bf = bf; f.M = Mp; f.D = D; f.NH = NH; f.cap = c.atten_logit_cap;
   f.hb = hb; f.big = big;
@@ -320,7 +319,7 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
                     sp_pos, Nsp, nullptr); }));
   }
   const double ln_bytes = dM * dD * dE + dM * dD * dE;
-  f.stats_part = fold;  // spatial layer 0's q|k|v GEMM combines the patch embedding's partials
+  if (fold) VP_HIP(f.finalize());
   auto run_stack = [&](std::vector<LayerW>& layers, void* xs, int num_seq, int S, const float* pad) -> int {
     const int acls = num_seq == (int)(B * T) ? PC_ATTN_SPATIAL : PC_ATTN_TEMPORAL;
     return f.run_stack(layers, xs, num_seq, S, pad, F, acls, ATT_VIDEO, bf, false);
@@ -336,8 +335,7 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
   VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
     return layernorm(x, bf, M, D, h->sln_g, h->sln_b, x2, bf, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s,
                      bf && c.num_temporal_layers > 0 ? ln_rs : nullptr); }));
-  // 4. temporal encoder over (b n) sequences of T tokens (spatial_ln wrote finalised statistics)
-  f.stats_part = false;
+  // 4. temporal encoder over (b n) sequences of T tokens
   if ((rc = run_stack(h->temporal, x2, (int)(B * Nsp), (int)T, pad_bnt))) return rc;
   // 5. temporal_ln and '(bn)td->b(tn)d'
   VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * dE + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
@@ -516,25 +514,6 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
   ep.pos = pos; ep.pos_rows = (int)(pos_rows > 0 ? pos_rows : 1); ep.rowpad = rowpad;
   ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.st_part = st_part; ep.st_rows = M;
-  VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
-                      static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-
-// Not in the public header: an LN-folded GEMM (EPI_BF16_LN / EPI_GELU_BF16_LN) that combines the
-// producers' partial statistics ln_part [ln_p][M][2] itself (tests: bitwise the ln_rs path after
-// ln_stats_finalize).
-int vp_dev_gemm_ln_part(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
-                        const float* bias, const float* ln_part, int64_t ln_p, const float* ln_c, const float* rowpad,
-                        void* stream) {
-  using namespace vp;
-  if (epi != EPI_BF16_LN && epi != EPI_GELU_BF16_LN) return fail(VP_EINVAL, "epilogue must be 8 or 9");
-  if (!ln_part || ln_p < 1 || ln_p > 8) return fail(VP_EINVAL, "ln_p must be 1..8");
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
-  EpiArgs ep;
-  ep.out = out; ep.ldo = N; ep.bias = bias; ep.rowpad = rowpad; ep.ln_c = ln_c;
-  ep.ln_part = ln_part; ep.ln_p = (int)ln_p; ep.ln_rows = M;
   VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
                       static_cast<hipStream_t>(stream)));
   return VP_OK;

@@ -478,10 +478,6 @@ struct Fwd {
   void* big = nullptr;       // [M][max(3D, F)] q|k|v, FFN hidden
   float* st_part = nullptr;  // [D/128][M][2] partial row statistics (folded LayerNorm)
   float* ln_rs = nullptr;    // [M][2] (rstd, -mean*rstd)
-  // the residual stream's LayerNorm statistics are still the producers' partials in st_part: the
-  // LN-folded GEMMs combine them themselves (EpiArgs::ln_part); only the fused temporal launches
-  // need them finalised into ln_rs
-  bool stats_part = false;
   Profiler* pf = nullptr;
 
   // profiled launch: records events around `fn` when vp_profile_enable() is active
@@ -510,9 +506,6 @@ struct Fwd {
     ep.out = o; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldo;
     ep.pos = pos; ep.pos_rows = pos_rows; ep.rowpad = rowpad;
     ep.ln_rs = ln_rs; ep.ln_c = lnc; ep.st_part = st_part; ep.st_rows = M;
-    if (bf && stats_part && (epi == vp::EPI_BF16_LN || epi == vp::EPI_GELU_BF16_LN)) {
-      ep.ln_part = st_part; ep.ln_p = D / 128; ep.ln_rows = M;
-    }
     if (bf) return vp::gemm_bf16_auto(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wt, K, M, N, K, ep, s);
     return vp::gemm_f32(epi, (const float*)A, K, (const float*)Wt, K, M, N, K, ep, s);
   }
@@ -520,7 +513,6 @@ struct Fwd {
   // (rstd, -mean*rstd) of the residual stream from the producers' partial statistics
   hipError_t finalize() {
     const double b = (double)M * (D / 128) * 8.0 + (double)M * 8.0;
-    stats_part = false;
     return rec(PC_LAYERNORM, 0.0, b, [&] { return vp::ln_stats_finalize(st_part, D / 128, M, ln_rs, s); });
   }
 
@@ -549,7 +541,6 @@ struct Fwd {
       LayerW& lw = layers[li];
       const bool last = li + 1 == layers.size();
       if (tattn) {
-        if (stats_part) VP_HIP(finalize());  // these two launches read (rstd, -mean*rstd) rows
         // P (normalised bf16 probabilities, 512 B per (sequence, head)) goes to `big`; O to hb
         vp::EpiArgs ep;
         ep.ln_rs = ln_rs; ep.cap = cap; ep.heads = NH;
@@ -596,8 +587,8 @@ struct Fwd {
       VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {
         return gemm(fold ? EPI_RESID_BF16_ST : epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1,
                     nullptr); }));
-      if (fold) {  // LN2 folded into ffn_layer1 (which combines post's partial statistics itself)
-        stats_part = true;
+      if (fold) {  // LN2 folded into ffn_layer1
+        VP_HIP(finalize());
         VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
           return gemm(EPI_GELU_BF16_LN, xs, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad, lw.c1); }));
       } else {
@@ -611,7 +602,7 @@ struct Fwd {
       VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, dE, dE), [&] {
         return gemm(st ? EPI_RESID_FFN_BF16_ST : epi_resid_ffn, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1,
                     pad); }));
-      if (st) stats_part = true;
+      if (st) VP_HIP(finalize());
     }
     return VP_OK;
   }

@@ -63,12 +63,6 @@ struct EpiArgs {
   int pos_rows = 1;
   const float* rowpad = nullptr;  // optional [M], 1 = padded token
   const float* ln_rs = nullptr;   // EPI_*_LN: [M][2] (rstd, -mean*rstd)
-  // EPI_BF16_LN / EPI_GELU_BF16_LN (4-wave kernel): instead of ln_rs, the producers' partial row
-  // statistics [ln_p][ln_rows][2] (sum, M2 over 128 columns each), combined in the consumer
-  // (ln_combine: bitwise what ln_stats_finalize writes), so no finalize launch sits between them
-  const float* ln_part = nullptr;
-  int ln_p = 0;
-  int64_t ln_rows = 0;
   const float* ln_c = nullptr;    // EPI_*_LN: [N] column sums of W'
   float* st_part = nullptr;       // EPI_*_ST: [N/128][M][2] partial (sum, M2) of each row
   int64_t st_rows = 0;            // EPI_*_ST: M (partial stride)

@@ -141,8 +141,6 @@ _SIGNATURES = {
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "vp_dev_patch_embed": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
-    "vp_dev_gemm_ln_part": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
-                                    c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "vp_dev_gemm_tattn": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
@@ -282,15 +280,6 @@ def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln
     call("vp_dev_gemm_ln", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
          _ptr(pos), pos.shape[0] if pos is not None else 0, _ptr(rowpad), _ptr(ln_rs), _ptr(ln_c),
          _ptr(st_part), _stream(stream))
-    return out
-
-
-def dev_gemm_ln_part(a, w, bias, epilogue, out, ln_part, ln_c, rowpad=None, stream=None):
-    """LN-folded bf16 w4 GEMM (8, 9) that combines partial row statistics ln_part [P][M][2] itself."""
-    M, K = a.shape
-    N = w.shape[0]
-    call("vp_dev_gemm_ln_part", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(ln_part),
-         ln_part.shape[0], _ptr(ln_c), _ptr(rowpad), _stream(stream))
     return out
 
 
