@@ -88,7 +88,8 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
-// accumulators stay live).
+// accumulators stay live); 16 = the LN-folded epilogues' row statistics not loaded (prices their
+// place at the head of each tile's vmcnt queue).
 
 // the LN fold of 4 accumulator values (r * a + (m * c + b)) in packed pairs: two IEEE fmas per value
 // (the scalar form is bitwise equal and measured no faster beside the fused epilogues' MFMAs:
@@ -352,7 +353,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
           for (int pass = 0; pass < 2; ++pass)
-            rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
+            rs[mt][pass] = (ABL & 16) ? make_float2(ep.cap, ep.cap_c1)
+                                      : *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
     if constexpr (EpiTraits<EPI>::kVAttn || EpiTraits<EPI>::kQkAttn) {  // last K-tile peeled (K >= 2 BK)
