@@ -207,7 +207,8 @@ def tattn(dev, g):
 def lnrs(dev, g):
     """The LN-folded GEMMs (q|k|v, ffn_layer1 at the bench shape) against their builds that skip the
     tile-start row-statistics loads (diag ABL 16): what those loads cost at the head of every tile's
-    vmcnt queue.  Interleaved rounds."""
+    vmcnt queue; and the build that requests the next tile's rows at the epilogue's start (ABL 32).
+    Interleaved rounds."""
     for which, name, N in ((0, "qkv", 2304), (1, "ffn1", 3072)):
         M, K = M_TOK, 768
         a, w, b = operands(M, N, K, g, dev)
@@ -217,11 +218,18 @@ def lnrs(dev, g):
         st = lambda: torch.cuda.current_stream().cuda_stream
         run = lambda abl: nat.call("vp_dev_gemm_ln_abl", which, abl, a.data_ptr(), w.data_ptr(), M, N, K, o.data_ptr(),
                                    b.data_ptr(), rs.data_ptr(), c.data_ptr(), st())
-        res = {k: [] for k in (0, 16)}
+        outs = {}
+        for k in (0, 32):
+            run(k)
+            torch.cuda.synchronize()
+            outs[k] = o.clone()
+        res = {k: [] for k in (0, 16, 32)}
         for _ in range(4):
             for k in res:
                 res[k].append(timeit(lambda: run(k)))
-        print(f"{name}: with row statistics {min(res[0])*1e3:7.1f} us | without {min(res[16])*1e3:7.1f} us", flush=True)
+        print(f"{name}: with row statistics {min(res[0])*1e3:7.1f} us | without {min(res[16])*1e3:7.1f} us | "
+              f"next tile's requested at the epilogue {min(res[32])*1e3:7.1f} us (bitwise {torch.equal(outs[0], outs[32])})",
+              flush=True)
         del a, o
 
 
