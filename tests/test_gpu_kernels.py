@@ -363,6 +363,47 @@ def _ln_ref(x, gamma1p, beta):
     return (x - m) / torch.sqrt(v + 1e-6) * gamma1p + beta
 
 
+@pytest.mark.parametrize("padded", [False, True])
+@pytest.mark.parametrize("M,D,F", [(2048, 768, 3072), (512, 1024, 4096)])
+def test_ffn_pair_row_blocked_bitwise(cuda, padded, M, D, F):
+    """The FFN pair over the row-blocked hidden activation (ffn_layer1 stores from the accumulator
+    layout with W1's rows permuted, ffn_layer2 stages A from the blocks) is bitwise the row-major
+    pair: the hidden activation is the row-major one re-laid, the output and its row statistics equal."""
+    g = torch.Generator(device="cpu").manual_seed(M + F + padded)
+    x = _bf(torch.randn(M, D, generator=g) * 2 + 0.5)
+    w1 = _bf(torch.randn(F, D, generator=g) / D ** 0.5)
+    b1 = torch.randn(F, generator=g) * 0.1
+    c1 = w1.double().sum(1).float()
+    w2 = _bf(torch.randn(D, F, generator=g) / F ** 0.5)
+    b2 = torch.randn(D, generator=g) * 0.1
+    pad = (torch.rand(M, generator=g) < 0.2).float().to(cuda) if padded else None
+    rs = torch.empty(M, 2, device=cuda)
+    xd = x.to(cuda)
+    nat.dev_ln_stats(xd, M, D, rs, from_partials=False)
+    perm = torch.from_numpy(nat.ffn1_blk_rows(F))
+    r0 = torch.randn(M, D, generator=g).to(torch.bfloat16).to(cuda)
+    h_rm = torch.empty(M, F, device=cuda, dtype=torch.bfloat16)
+    h_bk = torch.empty_like(h_rm)
+    nat.dev_gemm_ln(xd, w1.to(cuda), b1.to(cuda), nat.EPI_GELU_LN, h_rm, rowpad=pad, ln_rs=rs, ln_c=c1.to(cuda))
+    nat.dev_gemm_ln(xd, w1[perm].contiguous().to(cuda), b1[perm].to(cuda), nat.EPI_GELU_LN_BLK, h_bk, rowpad=pad,
+                    ln_rs=rs, ln_c=c1[perm].to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(h_bk, nat.to_row_blocked(h_rm))
+    y_rm, y_bk = r0.clone(), r0.clone()
+    st_rm = torch.empty(D // 128, M, 2, device=cuda)
+    st_bk = torch.empty_like(st_rm)
+    nat.dev_gemm_ln(h_rm, w2.to(cuda), b2.to(cuda), nat.EPI_RESID_FFN_BF16_ST, y_rm, resid=y_rm, rowpad=pad,
+                    st_part=st_rm)
+    nat.dev_gemm_ln(h_bk, w2.to(cuda), b2.to(cuda), nat.EPI_RESID_FFN_BF16_ST_BLK, y_bk, resid=y_bk, rowpad=pad,
+                    st_part=st_bk)
+    z_rm, z_bk = r0.clone(), r0.clone()
+    nat.dev_gemm_kernel(4, h_rm, w2.to(cuda), b2.to(cuda), nat.EPI_RESID_FFN_BF16, z_rm, resid=z_rm, rowpad=pad)
+    nat.dev_gemm_ln(h_bk, w2.to(cuda), b2.to(cuda), nat.EPI_RESID_FFN_BF16_BLK, z_bk, resid=z_bk, rowpad=pad)
+    torch.cuda.synchronize()
+    assert torch.equal(y_rm, y_bk) and torch.equal(st_rm, st_bk)
+    assert torch.equal(z_rm, z_bk)
+
+
 @pytest.mark.parametrize("epi", [nat.EPI_BF16_LN, nat.EPI_GELU_LN])
 @pytest.mark.parametrize("M,N,K", [(1024, 2304, 768), (512, 3072, 768), (256, 1024, 1024)])
 def test_gemm_ln_fold(cuda, epi, M, N, K):

@@ -57,6 +57,20 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       return launch_w4<EPI_RESID_FFN_BF16_ST, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_POS_BF16_ST: return launch_w4<EPI_POS_BF16_ST, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RELU_BF16: return launch_w4<EPI_RELU_BF16, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
+    // the FFN pair over the row-blocked hidden activation (vp_kernels.h EPI_*_BLK): row-major A / W
+    // for ffn_layer1, A blocked for ffn_layer2 (lda = K, K % 64 == 0)
+    case EPI_GELU_BF16_LN_BLK:
+      if (N % 32 || ldw != K) return hipErrorInvalidValue;
+      if (!ep.rowpad) return launch_w4<EPI_GELU_BF16_LN_BLK, true, S2>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_GELU_BF16_LN_BLK, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16_ST_BLK:
+      if (lda != K) return hipErrorInvalidValue;
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, S3>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_RESID_FFN_BF16_BLK:
+      if (lda != K) return hipErrorInvalidValue;
+      if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_BLK, false, S3>(A, lda, W, ldw, M, N, K, ep, s);
+      return launch_w4<EPI_RESID_FFN_BF16_BLK, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     // temporal layers' q|k|v projection with the attention fused (T = 16): S3 as the q|k|v GEMM
     // (their last K-tile is peeled: K >= 2 BK)
     case EPI_QK_TATTN_LN:

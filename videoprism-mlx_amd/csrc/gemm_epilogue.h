@@ -20,11 +20,16 @@ namespace vp {
 template <int EPI>
 struct EpiTraits {
   static constexpr bool kLn = EPI == EPI_BF16_LN || EPI == EPI_GELU_BF16_LN;
-  static constexpr bool kStats = EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST || EPI == EPI_POS_BF16_ST;
-  static constexpr bool kGelu = EPI == EPI_GELU_BF16 || EPI == EPI_GELU_BF16_LN;
+  static constexpr bool kStats = EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST || EPI == EPI_POS_BF16_ST ||
+                                 EPI == EPI_RESID_FFN_BF16_ST_BLK;
+  static constexpr bool kGelu = EPI == EPI_GELU_BF16 || EPI == EPI_GELU_BF16_LN || EPI == EPI_GELU_BF16_LN_BLK;
   static constexpr bool kResidF32 = EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN;
   static constexpr bool kResidBf16 = EPI == EPI_RESID_BF16 || EPI == EPI_RESID_FFN_BF16 ||
-                                     EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST;
+                                     EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST ||
+                                     EPI == EPI_RESID_FFN_BF16_ST_BLK || EPI == EPI_RESID_FFN_BF16_BLK;
+  // the FFN pair over the row-blocked hidden activation (vp_kernels.h EPI_*_BLK)
+  static constexpr bool kBlkOut = EPI == EPI_GELU_BF16_LN_BLK;
+  static constexpr bool kABlk = EPI == EPI_RESID_FFN_BF16_ST_BLK || EPI == EPI_RESID_FFN_BF16_BLK;
   static constexpr bool kPos = EPI == EPI_POS_F32 || EPI == EPI_POS_BF16 || EPI == EPI_POS_BF16_ST;
   static constexpr bool kExtra = kResidF32 || kResidBf16 || kPos;
   // residual-stream producers (bf16 path): their A (the attention output / the FFN hidden activation)
@@ -32,7 +37,8 @@ struct EpiTraits {
   // is stored with default-policy (cache-allocating) stores -- the next readers of the residual stream
   // (the LN-folded consumer GEMM, the next residual epilogue) then find it in the Infinity Cache, which
   // the once-read streams (q|k|v, attention output, hidden activation) no longer displace
-  static constexpr bool kResidStream = EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST;
+  static constexpr bool kResidStream = EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST ||
+                                       EPI == EPI_RESID_FFN_BF16_ST_BLK;
   static constexpr bool kRelu = EPI == EPI_RELU_BF16;
   static constexpr bool kKeep = kGelu || kRelu || kResidF32 || kResidBf16;
   static constexpr bool kOutBf16 = !(EPI == EPI_RESID_F32 || EPI == EPI_RESID_FFN || EPI == EPI_POS_F32);

@@ -172,7 +172,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     const int vo = jj >= av_cpr ? 0 : min(8 * jj, 3 * av_p - 8);
     return prow * prow_b + (uint32_t)vo * 2;
   };
-  const uint32_t vA[2] = {AVID ? video_off(0) : prow * a_rb + cE, AVID ? video_off(1) : prow * a_rb + cO};
+  // ABLK (A = the row-blocked hidden activation [M/16][K/32][16][32]): logical chunk j of a piece row
+  // is 16 B of column block j >> 2 (1 KiB apart), row (piece parity * 8 + prow) of the block (64 B)
+  auto ablk_off = [&](int par) -> uint32_t {
+    const uint32_t jj = (uint32_t)((lane & 7) ^ swz(prow + 8 * par));
+    return (jj >> 2) * 1024u + (uint32_t)prow * 64u + (jj & 3u) * 16u;
+  };
+  constexpr bool ABLK = EpiTraits<EPI>::kABlk;
+  const uint32_t vA[2] = {AVID ? video_off(0) : ABLK ? ablk_off(0) : prow * a_rb + cE,
+                          AVID ? video_off(1) : ABLK ? ablk_off(1) : prow * a_rb + cO};
   const uint32_t vW[2] = {prow * w_rb + cE, prow * w_rb + cO};
   typedef __attribute__((address_space(3))) void lds_void;
   // load stream: K-tile ld_g -> (tile ld_tm/ld_tn, K-tile ld_kt); the tail re-loads the last
@@ -201,6 +209,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       if constexpr (AVID) {  // piece w*8+i: patch-grid row (w*8+i) >> 1, patches 8 ((w*8+i) & 1) + 0..7
         const int pc = w * 8 + i;
         so = (uint32_t)ld_tm * frame_b + (uint32_t)((pc >> 1) * av_p + ld_kt) * a_rb + (uint32_t)(pc & 1) * 8 * prow_b;
+      } else if constexpr (ABLK) {  // piece rows 8 pc .. +7: block row pc >> 1, half pc & 1; K-tile = blocks 2 kt, +1
+        const int pc = w * 8 + i;
+        so = (uint32_t)((ld_tm * 16 + (pc >> 1)) * (K >> 5) + 2 * ld_kt) * 1024u + (uint32_t)(pc & 1) * 512u;
       } else {
         so = (uint32_t)(ld_tm * BM + (w * 8 + i) * 8) * a_rb + ld_kt * (BK * 2);
       }
@@ -350,6 +361,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     float4 bl[2], bh[2];
     float4 cl[2], ch[2];  // EPI_*_LN: column sums of W'
     float2 rs[8][2];      // EPI_*_LN: (rstd, -mean*rstd) of rows mt*16 + pass*8 + er
+    float2 rsb[8];        // EPI_GELU_BF16_LN_BLK: (rstd, -mean*rstd) of rows mt*16 + (lane & 15)
+    float keepb[8];       // EPI_GELU_BF16_LN_BLK with padded rows: 1 - rowpad of the same rows
     {
       int ttm, ttn;
       coords(first + j * stride, ttm, ttn);
@@ -358,6 +371,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       for (int nh = 0; nh < 2; ++nh) {
         bl[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64);
         bh[nh] = *reinterpret_cast<const float4*>(ep.bias + nb + nh * 64 + 4);
+      }
+      if constexpr (EpiTraits<EPI>::kBlkOut) {
+        const int rb = ttm * BM + wm * 128 + (lane & 15);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          rsb[mt] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(rb + mt * 16));
+          if constexpr (!NOPAD) keepb[mt] = 1.0f - ep.rowpad[rb + mt * 16];
+        }
       }
       if constexpr (EpiTraits<EPI>::kLn) {  // (the fused temporal epilogues load theirs in the epilogue)
 #pragma unroll
@@ -410,6 +431,51 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     using Tr = EpiTraits<EPI>;
     // S3: the A buffer of the tile's last K-tile (free since its h1 barrier; refilled in the next h0)
     char* scr = (S3 ? a_buf(a3 == 0 ? 2 : a3 - 1) : smem + kLds) + w * kScr;
+    if constexpr (Tr::kBlkOut) {
+      // ---- ffn_layer1 into the row-blocked hidden activation (vp_kernels.h EPI_GELU_BF16_LN_BLK): the
+      // LN fold + GELU where the accumulators stand (lane: row r16 of block mt, W rows 16 nt + 4 g4 ..
+      // +3), the same IEEE operations as the row-major epilogue; nt pair (2p, 2p+1) gives the lane 8
+      // natural columns 32 p + 8 g4 .. +7 (host row permutation), stored as 16 B at row r16 of the
+      // 1 KiB block (row block, column block) -- one whole block per store instruction
+      int lid = lane;
+      asm volatile("" : "+v"(lid));
+      const int r16 = lid & 15, g4 = lid >> 4;
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+a"(acc[nt][mt]));
+      char* lc = scr;  // c at +0, b' at +512 (the wave's 128 W rows)
+      {
+        const float* src = (lid < 32 ? ep.ln_c : ep.bias) + n0 + 4 * (lid & 31);
+        *reinterpret_cast<float4*>(lc + (lid < 32 ? 0 : 512) + 16 * (lid & 31)) = *reinterpret_cast<const float4*>(src);
+      }
+      const int64_t nblk = N >> 5;
+      bf16_t* outp = static_cast<bf16_t*>(ep.out);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float4 c0 = *reinterpret_cast<const float4*>(lc + 4 * (32 * p + 4 * g4));
+        const float4 c1 = *reinterpret_cast<const float4*>(lc + 4 * (32 * p + 16 + 4 * g4));
+        const float4 b0 = *reinterpret_cast<const float4*>(lc + 512 + 4 * (32 * p + 4 * g4));
+        const float4 b1 = *reinterpret_cast<const float4*>(lc + 512 + 4 * (32 * p + 16 + 4 * g4));
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          f32x2_t v[4];
+          fold4(acc[2 * p][mt], rsb[mt].x, rsb[mt].y, c0, b0, v[0], v[1]);
+          fold4(acc[2 * p + 1][mt], rsb[mt].x, rsb[mt].y, c1, b1, v[2], v[3]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[q] = gelu_fast2(v[q]);
+            if constexpr (!NOPAD) v[q] = v[q] * f32x2_t(keepb[mt]);
+          }
+          const uint4 pk = make_uint4(pack_bf16x2(v[0].x, v[0].y), pack_bf16x2(v[1].x, v[1].y),
+                                      pack_bf16x2(v[2].x, v[2].y), pack_bf16x2(v[3].x, v[3].y));
+          const int64_t blk = (int64_t)((m0 >> 4) + mt) * nblk + ((n0 >> 5) + p);
+          st_nt(outp + blk * 512 + r16 * 32 + 8 * g4, pk);
+          __builtin_amdgcn_sched_barrier(0);  // one block's accumulator reads at a time
+        }
+      }
+      continue;  // nothing else of this tile is stored
+    }
     if constexpr (Tr::kQkAttn || Tr::kVAttn) {
       // ---- fused temporal attention (EPI_QK_TATTN_LN / EPI_V_TATTN_LN, see vp_kernels.h).  A
       // 16-row block mt of this wave's 128 rows is one (b n) sequence of T = 16 frames; the

@@ -501,13 +501,15 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
 
 // Not in the public header: the GEMM-folded LayerNorm pieces (tests/test_gpu_kernels.py).
 // vp_dev_gemm_ln: EPI_BF16_LN / EPI_GELU_BF16_LN with (rstd, -mean*rstd) rows ln_rs and column
-// sums ln_c, or EPI_*_ST writing partial row statistics to st_part ([N/128][M][2]).
+// sums ln_c, or EPI_*_ST writing partial row statistics to st_part ([N/128][M][2]); EPI_*_BLK: the FFN
+// pair over the row-blocked hidden activation (vp_kernels.h).
 int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
                    const float* bias, const void* resid, const float* pos, int64_t pos_rows,
                    const float* rowpad, const float* ln_rs, const float* ln_c, float* st_part,
                    void* stream) {
   using namespace vp;
-  if (epi < EPI_BF16_LN || epi > EPI_POS_BF16_ST) return fail(VP_EINVAL, "epilogue must be 8..12");
+  if (!((epi >= EPI_BF16_LN && epi <= EPI_POS_BF16_ST) || (epi >= EPI_GELU_BF16_LN_BLK && epi <= EPI_RESID_FFN_BF16_BLK)))
+    return fail(VP_EINVAL, "epilogue must be 8..12 or 16..18");
   const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;

@@ -97,6 +97,9 @@ struct LayerW {  // one transformer layer, packed
   void* wqk = nullptr;
   float* bqk = nullptr;
   float* cqk = nullptr;
+  // bf16, folded, F % 256 == 0: w1 / b1 / c1 rows permuted within each 32-row group (W row 16h + 4g + i
+  // holds column 8g + 4h + i) for the FFN pair over the row-blocked hidden activation (EPI_*_BLK)
+  bool ffn_blk = false;
 };
 
 constexpr int kMaxT = 32;
@@ -347,7 +350,20 @@ int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH
     std::vector<float> bb1(b1.begin() + (size_t)l * F, b1.begin() + (size_t)(l + 1) * F);
     std::vector<float> bb2(b2.begin() + (size_t)l * D, b2.begin() + (size_t)(l + 1) * D);
     if (fold) {
-      const std::vector<float> c = fold_ln(t1, bb1, g2, be2, F, D);
+      std::vector<float> c = fold_ln(t1, bb1, g2, be2, F, D);
+      if (F % 256 == 0) {  // rows of W', b', c in the blocked FFN pair's order (LayerW::ffn_blk)
+        std::vector<float> pt((size_t)F * D), pb(F), pc(F);
+        for (int64_t r = 0; r < F; ++r) {
+          const int64_t w = r & 31, src = (r & ~31LL) + 8 * ((w >> 2) & 3) + 4 * (w >> 4) + (w & 3);
+          std::memcpy(pt.data() + (size_t)r * D, t1.data() + (size_t)src * D, (size_t)D * 4);
+          pb[r] = bb1[src];
+          pc[r] = c[src];
+        }
+        t1.swap(pt);
+        bb1.swap(pb);
+        c.swap(pc);
+        lw.ffn_blk = true;
+      }
       if ((rc = upload_f32(h, c, &lw.c1))) return rc;
     }
     if ((rc = upload_mat(h, t1, &lw.w1)) || (rc = upload_f32(h, bb1, &lw.b1)) ||
@@ -590,7 +606,8 @@ struct Fwd {
       if (fold) {  // LN2 folded into ffn_layer1
         VP_HIP(finalize());
         VP_HIP(rec(PC_GEMM_FFN1, 2.0 * dM * dD * dF, gbytes(dD, dF, dE, 0), [&] {
-          return gemm(EPI_GELU_BF16_LN, xs, D, lw.w1, F, big, F, lw.b1, nullptr, nullptr, 1, pad, lw.c1); }));
+          return gemm(lw.ffn_blk ? EPI_GELU_BF16_LN_BLK : EPI_GELU_BF16_LN, xs, D, lw.w1, F, big, F, lw.b1, nullptr,
+                      nullptr, 1, pad, lw.c1); }));
       } else {
         VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
           return layernorm(xs, xbf, M, D, lw.ln2_g, lw.ln2_b, hb, bf, PERM_NONE, 1, 1, nullptr, s); }));
@@ -599,9 +616,10 @@ struct Fwd {
                       pad); }));
       }
       const bool st = fold && !last;  // the next layer's LN1 statistics
+      const int epi_ffn2 = lw.ffn_blk && fold ? (st ? EPI_RESID_FFN_BF16_ST_BLK : EPI_RESID_FFN_BF16_BLK)
+                                              : st ? EPI_RESID_FFN_BF16_ST : epi_resid_ffn;
       VP_HIP(rec(PC_GEMM_FFN2, 2.0 * dM * dF * dD, gbytes(dF, dD, dE, dE), [&] {
-        return gemm(st ? EPI_RESID_FFN_BF16_ST : epi_resid_ffn, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1,
-                    pad); }));
+        return gemm(epi_ffn2, big, F, lw.w2, D, xs, D, lw.b2, xs, nullptr, 1, pad); }));
       if (st) VP_HIP(finalize());
     }
     return VP_OK;

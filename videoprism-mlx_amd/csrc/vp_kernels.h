@@ -51,6 +51,15 @@ enum Epilogue {
   //    [M][D] comes out of the GEMM and q|k|v never reach HBM.
   EPI_QK_TATTN_LN = 14,
   EPI_V_TATTN_LN = 15,
+  // The FFN pair with the hidden activation h in a row-blocked layout [M/16][F/32][16][32] (4-wave
+  // kernel, bf16): ffn_layer1's epilogue stores straight from the accumulator layout -- a lane's
+  // 8 values of one row are 8 natural columns because W1's rows (and b', c) are permuted within each
+  // 32-row group on the host (W-row 16h + 4g + i holds column 8g + 4h + i), and one store
+  // instruction writes one whole 1 KiB block -- so no LDS transposition; ffn_layer2 stages its A
+  // K-tiles from that layout.  Bitwise the row-major pair.
+  EPI_GELU_BF16_LN_BLK = 16,       // ffn_layer1 (as EPI_GELU_BF16_LN), h blocked
+  EPI_RESID_FFN_BF16_ST_BLK = 17,  // ffn_layer2 (as EPI_RESID_FFN_BF16_ST), A = blocked h
+  EPI_RESID_FFN_BF16_BLK = 18,     // ffn_layer2 (as EPI_RESID_FFN_BF16), A = blocked h
 };
 
 struct EpiArgs {

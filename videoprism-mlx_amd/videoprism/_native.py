@@ -271,6 +271,23 @@ def dev_gemm_kernel(which, a, w, bias, epilogue, out, resid=None, pos=None, rowp
 
 
 EPI_BF16_LN, EPI_GELU_LN, EPI_RESID_BF16_ST, EPI_RESID_FFN_BF16_ST, EPI_POS_BF16_ST = 8, 9, 10, 11, 12
+# the FFN pair over the row-blocked hidden activation [M/16][F/32][16][32] (vp_kernels.h EPI_*_BLK)
+EPI_GELU_LN_BLK, EPI_RESID_FFN_BF16_ST_BLK, EPI_RESID_FFN_BF16_BLK = 16, 17, 18
+
+
+def ffn1_blk_rows(F):
+    """Row order of W1 / b' / c for EPI_GELU_LN_BLK (vp_internal.h pack_stack): packed row r holds
+    natural row src[r] -- within each 32-row group, row 16 h + 4 g + i holds column 8 g + 4 h + i."""
+    import numpy as np
+    r = np.arange(F)
+    w = r & 31
+    return (r & ~31) + 8 * ((w >> 2) & 3) + 4 * (w >> 4) + (w & 3)
+
+
+def to_row_blocked(h):
+    """[M, F] row-major -> the [M/16][F/32][16][32] blocked layout, flattened back to [M, F] storage."""
+    M, F = h.shape
+    return h.reshape(M // 16, 16, F // 32, 32).permute(0, 2, 1, 3).reshape(M, F)
 
 
 def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln_rs=None,
