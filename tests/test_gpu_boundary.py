@@ -85,7 +85,7 @@ def test_profile_kernel_symbol(cuda):
     eng.profile_enable(0)
     names = {c: eng.kernel_name(c) for c in ("gemm_ffn1_gelu", "gemm_qkv", "attention_spatial")}
     print(names)
-    assert names["gemm_ffn1_gelu"].startswith("gemm_bf16_w4_kernel<9")
+    assert names["gemm_ffn1_gelu"].startswith("gemm_bf16_w4_kernel<16")  # EPI_GELU_BF16_LN_BLK
     assert names["gemm_qkv"].startswith("gemm_bf16_w4_kernel<8")
     assert names["attention_spatial"].startswith("attn_spatial_kernel<")
 
