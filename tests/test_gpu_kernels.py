@@ -363,6 +363,38 @@ def _ln_ref(x, gamma1p, beta):
     return (x - m) / torch.sqrt(v + 1e-6) * gamma1p + beta
 
 
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("frames,D", [(6, 768), (3, 1024)])
+def test_qkv_spatial_attention_row_blocked_bitwise(cuda, masked, frames, D):
+    """The spatial layers' q|k|v projection into the row-blocked layout (EPI_BF16_LN_BLK, rows of Wqkv /
+    b' / c permuted within 32-row groups) and the spatial attention reading it are bitwise the row-major
+    pair: q|k|v re-laid equal, attention output equal (with and without padded keys)."""
+    M, NH = frames * 256, D // 64
+    g = torch.Generator(device="cpu").manual_seed(frames + D + masked)
+    x = _bf(torch.randn(M, D, generator=g) * 2 + 0.5)
+    w = _bf(torch.randn(3 * D, D, generator=g) / D ** 0.5)
+    b = torch.randn(3 * D, generator=g) * 0.1
+    c = w.double().sum(1).float()
+    xd = x.to(cuda)
+    rs = torch.empty(M, 2, device=cuda)
+    nat.dev_ln_stats(xd, M, D, rs, from_partials=False)
+    perm = torch.from_numpy(nat.ffn1_blk_rows(3 * D))
+    q_rm = torch.empty(M, 3 * D, device=cuda, dtype=torch.bfloat16)
+    q_bk = torch.empty_like(q_rm)
+    nat.dev_gemm_ln(xd, w.to(cuda), b.to(cuda), nat.EPI_BF16_LN, q_rm, ln_rs=rs, ln_c=c.to(cuda))
+    nat.dev_gemm_ln(xd, w[perm].contiguous().to(cuda), b[perm].to(cuda), nat.EPI_BF16_LN_BLK, q_bk, ln_rs=rs,
+                    ln_c=c[perm].to(cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(q_bk, nat.to_row_blocked(q_rm))
+    kp = (torch.rand(M, generator=g) < 0.3).float().to(cuda) if masked else None
+    o_rm = nat.op_attention(q_rm, frames, 256, NH, 50.0, key_pad=kp)
+    o_bk = torch.empty_like(o_rm)
+    nat.call("vp_dev_attention_spatial_blk", q_bk.data_ptr(), o_bk.data_ptr(), frames, NH, 50.0,
+             kp.data_ptr() if kp is not None else None, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(o_rm, o_bk)
+
+
 @pytest.mark.parametrize("padded", [False, True])
 @pytest.mark.parametrize("M,D,F", [(2048, 768, 3072), (512, 1024, 4096)])
 def test_ffn_pair_row_blocked_bitwise(cuda, padded, M, D, F):

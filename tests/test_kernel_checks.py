@@ -59,7 +59,7 @@ def test_product_kernels_no_scratch_no_spills():
     by = {k[".name"]: k for k in ks}
     spatial = [n for n in by if "attn_spatial_kernel" in n]
     long_ = [n for n in by if "attn_long_kernel" in n]
-    assert len(spatial) == 2 and len(long_) == 1
+    assert len(spatial) == 4 and len(long_) == 1  # (masked or not) x (row-major or row-blocked q|k|v)
     # attn_long_kernel runs two 512-thread workgroups per CU: 128 VGPRs per lane at most
     assert int(by[long_[0]][".vgpr_count"]) <= 128
 

@@ -56,7 +56,10 @@ constexpr int kSpLds = 2 * kSpS * 128 + kSpS * 4 + 16;
 // segments (8 rows per store); O is written with nontemporal stores (read once, by the post
 // projection), so it does not displace the residual stream from the Infinity Cache (gemm_epilogue.h
 // kResidStream).  (Nontemporal q|k|v loads measured slower: 2.45 vs 2.37-2.40 ms per step.)
-template <bool MASK>
+// BLK: q|k|v in the row-blocked layout of the q|k|v GEMM's EPI_BF16_LN_BLK ([M/16][3D/32][16][32],
+// element (row, col) at ((row >> 4) * 3D/32 + (col >> 5)) * 512 + (row & 15) * 32 + (col & 31)): a K / V
+// piece (8 keys x 64 dims) is then two 512-B runs instead of 8 rows of 128 B
+template <bool MASK, bool BLK = false>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     const bf16_t* __restrict__ qkv, bf16_t* __restrict__ o, int heads, float cap,
     const float* __restrict__ key_pad, int rev, int64_t rs, int64_t hs, int64_t sec) {
@@ -76,6 +79,10 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   const int lane = threadIdx.x & 63;
   const int w = wave_id();
   const bf16_t* base = qkv + (int64_t)seq * kSpS * ld + h * hs;
+  // BLK: element (row r of this sequence, column col of the q|k|v row)
+  auto blk_at = [&](int r, int col) {
+    return qkv + (((int64_t)seq * 16 + (r >> 4)) * (ld >> 5) + (col >> 5)) * 512 + (r & 15) * 32 + (col & 31);
+  };
 
   // ---- this wave's 32 queries as the B operand (lane: q = l&31, d = 16kd + 8(l>>5) + j),
   // requested ahead of the K/V stream.  hipcc cannot count a plain load against the LDS-DMA
@@ -90,8 +97,10 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   {
     const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
 #pragma unroll
-    for (int kd = 0; kd < 4; ++kd)
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qp + 16 * kd));
+    for (int kd = 0; kd < 4; ++kd) {
+      const bf16_t* qa = BLK ? blk_at(q0 + (lane & 31), h * 64 + 16 * kd + 8 * half) : qp + 16 * kd;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qa));
+    }
   }
   // ---- stage K and V in 4 chunks of 64 keys, chunk-major: wave w loads K piece c*8+w and
   // V piece 32+c*8+w of chunk c (a piece = 8 keys x 128 B), so key tiles 2c, 2c+1 can start as
@@ -103,7 +112,8 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
       const int piece = isV * 32 + cc * 8 + w;
       const int row = (piece & 31) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
-      const bf16_t* src = base + (int64_t)row * ld + (isV ? 2 * sec : sec) + c * 8;
+      const bf16_t* src = BLK ? blk_at(row, (isV ? 2 : 1) * (int)sec + h * 64 + c * 8)
+                              : base + (int64_t)row * ld + (isV ? 2 * sec : sec) + c * 8;
       __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
     }
   if constexpr (MASK) {  // (padded batches: no streaming)
@@ -421,11 +431,13 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
 }  // namespace
 
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads, float cap,
-                                  const float* key_pad, hipStream_t s) {
+                                  const float* key_pad, hipStream_t s, bool blk) {
   if (!(cap > 0.0f)) return hipErrorInvalidValue;
-  static bool attr[2] = {false, false};
-  const int mi = key_pad ? 1 : 0;
-  const void* fn = key_pad ? (const void*)attn_spatial_kernel<true> : (const void*)attn_spatial_kernel<false>;
+  static bool attr[4] = {false, false, false, false};
+  const int mi = (key_pad ? 1 : 0) + (blk ? 2 : 0);
+  const void* fns[4] = {(const void*)attn_spatial_kernel<false, false>, (const void*)attn_spatial_kernel<true, false>,
+                        (const void*)attn_spatial_kernel<false, true>, (const void*)attn_spatial_kernel<true, true>};
+  const void* fn = fns[mi];
   if (!attr[mi]) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
     if (e != hipSuccess) return e;
@@ -441,13 +453,18 @@ hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int
   // O leaves through LDS as whole 128-B row segments (217 -> 209 us at the bench shape); a
   // head-major q|k|v layout measured only 1 % faster and is not used
   const int64_t D = heads * 64;
+  if (blk && (3 * D) % 32) return hipErrorInvalidValue;
   VP_NOTE_KERNEL(fn);
-  if (key_pad)
-    hipLaunchKernelGGL(attn_spatial_kernel<true>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad,
-                       rev, 3 * D, (int64_t)64, D);
-  else
-    hipLaunchKernelGGL(attn_spatial_kernel<false>, grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad,
-                       rev, 3 * D, (int64_t)64, D);
+#define VP_SPATIAL(M, B)                                                                                        \
+  hipLaunchKernelGGL((attn_spatial_kernel<M, B>), grid, dim3(kSpThreads), kSpLds, s, qkv, o, heads, cap, key_pad, \
+                     rev, 3 * D, (int64_t)64, D)
+  switch (mi) {
+    case 0: VP_SPATIAL(false, false); break;
+    case 1: VP_SPATIAL(true, false); break;
+    case 2: VP_SPATIAL(false, true); break;
+    default: VP_SPATIAL(true, true); break;
+  }
+#undef VP_SPATIAL
   return hipGetLastError();
 }
 

@@ -63,6 +63,9 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
       if (N % 32 || ldw != K) return hipErrorInvalidValue;
       if (!ep.rowpad) return launch_w4<EPI_GELU_BF16_LN_BLK, true, S2>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_GELU_BF16_LN_BLK, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_BF16_LN_BLK:
+      if (N % 32 || ldw != K) return hipErrorInvalidValue;
+      return launch_w4<EPI_BF16_LN_BLK, true, S3>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_RESID_FFN_BF16_ST_BLK:
       if (lda != K) return hipErrorInvalidValue;
       if (K >= 2048) return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, S3>(A, lda, W, ldw, M, N, K, ep, s);

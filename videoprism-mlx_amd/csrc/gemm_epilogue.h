@@ -28,7 +28,7 @@ struct EpiTraits {
                                      EPI == EPI_RESID_BF16_ST || EPI == EPI_RESID_FFN_BF16_ST ||
                                      EPI == EPI_RESID_FFN_BF16_ST_BLK || EPI == EPI_RESID_FFN_BF16_BLK;
   // the FFN pair over the row-blocked hidden activation (vp_kernels.h EPI_*_BLK)
-  static constexpr bool kBlkOut = EPI == EPI_GELU_BF16_LN_BLK;
+  static constexpr bool kBlkOut = EPI == EPI_GELU_BF16_LN_BLK || EPI == EPI_BF16_LN_BLK;
   static constexpr bool kABlk = EPI == EPI_RESID_FFN_BF16_ST_BLK || EPI == EPI_RESID_FFN_BF16_BLK;
   static constexpr bool kPos = EPI == EPI_POS_F32 || EPI == EPI_POS_BF16 || EPI == EPI_POS_BF16_ST;
   static constexpr bool kExtra = kResidF32 || kResidBf16 || kPos;

@@ -377,7 +377,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
           rsb[mt] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(rb + mt * 16));
-          if constexpr (!NOPAD) keepb[mt] = 1.0f - ep.rowpad[rb + mt * 16];
+          if constexpr (EpiTraits<EPI>::kKeep && !NOPAD) keepb[mt] = 1.0f - ep.rowpad[rb + mt * 16];
         }
       }
       if constexpr (EpiTraits<EPI>::kLn) {  // (the fused temporal epilogues load theirs in the epilogue)
@@ -432,8 +432,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     // S3: the A buffer of the tile's last K-tile (free since its h1 barrier; refilled in the next h0)
     char* scr = (S3 ? a_buf(a3 == 0 ? 2 : a3 - 1) : smem + kLds) + w * kScr;
     if constexpr (Tr::kBlkOut) {
-      // ---- ffn_layer1 into the row-blocked hidden activation (vp_kernels.h EPI_GELU_BF16_LN_BLK): the
-      // LN fold + GELU where the accumulators stand (lane: row r16 of block mt, W rows 16 nt + 4 g4 ..
+      // ---- ffn_layer1 / the spatial q|k|v projection into a row-blocked layout (vp_kernels.h
+      // EPI_GELU_BF16_LN_BLK, EPI_BF16_LN_BLK): the LN fold (+ GELU) where the accumulators stand (lane: row r16 of block mt, W rows 16 nt + 4 g4 ..
       // +3), the same IEEE operations as the row-major epilogue; nt pair (2p, 2p+1) gives the lane 8
       // natural columns 32 p + 8 g4 .. +7 (host row permutation), stored as 16 B at row r16 of the
       // 1 KiB block (row block, column block) -- one whole block per store instruction
@@ -464,8 +464,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           fold4(acc[2 * p + 1][mt], rsb[mt].x, rsb[mt].y, c1, b1, v[2], v[3]);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            v[q] = gelu_fast2(v[q]);
-            if constexpr (!NOPAD) v[q] = v[q] * f32x2_t(keepb[mt]);
+            if constexpr (Tr::kGelu) v[q] = gelu_fast2(v[q]);
+            if constexpr (Tr::kKeep && !NOPAD) v[q] = v[q] * f32x2_t(keepb[mt]);
           }
           const uint4 pk = make_uint4(pack_bf16x2(v[0].x, v[0].y), pack_bf16x2(v[1].x, v[1].y),
                                       pack_bf16x2(v[2].x, v[2].y), pack_bf16x2(v[3].x, v[3].y));

@@ -508,8 +508,8 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
                    const float* rowpad, const float* ln_rs, const float* ln_c, float* st_part,
                    void* stream) {
   using namespace vp;
-  if (!((epi >= EPI_BF16_LN && epi <= EPI_POS_BF16_ST) || (epi >= EPI_GELU_BF16_LN_BLK && epi <= EPI_RESID_FFN_BF16_BLK)))
-    return fail(VP_EINVAL, "epilogue must be 8..12 or 16..18");
+  if (!((epi >= EPI_BF16_LN && epi <= EPI_POS_BF16_ST) || (epi >= EPI_GELU_BF16_LN_BLK && epi <= EPI_BF16_LN_BLK)))
+    return fail(VP_EINVAL, "epilogue must be 8..12 or 16..19");
   const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
@@ -518,6 +518,17 @@ int vp_dev_gemm_ln(int epi, const void* A, const void* W, int64_t M, int64_t N, 
   ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.st_part = st_part; ep.st_rows = M;
   VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep,
                       static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
+// Not in the public header: the spatial attention (S = 256) over q|k|v in the row-blocked layout of
+// EPI_BF16_LN_BLK (tests: bitwise the row-major path).
+int vp_dev_attention_spatial_blk(const void* qkv, void* o, int64_t num_seq, int64_t heads, float cap,
+                                 const float* key_pad, void* stream) {
+  using namespace vp;
+  if (!qkv || !o || num_seq < 1 || heads < 1) return fail(VP_EINVAL, "bad argument");
+  VP_HIP(attention_spatial_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)heads, cap, key_pad,
+                                static_cast<hipStream_t>(stream), true));
   return VP_OK;
 }
 

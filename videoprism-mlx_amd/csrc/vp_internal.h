@@ -100,6 +100,11 @@ struct LayerW {  // one transformer layer, packed
   // bf16, folded, F % 256 == 0: w1 / b1 / c1 rows permuted within each 32-row group (W row 16h + 4g + i
   // holds column 8g + 4h + i) for the FFN pair over the row-blocked hidden activation (EPI_*_BLK)
   bool ffn_blk = false;
+  // spatial stacks (bf16, folded, 3D % 256 == 0): a copy of wqkv / b' / c with the rows permuted the same
+  // way, for the q|k|v projection into the row-blocked layout the spatial attention reads (EPI_BF16_LN_BLK)
+  void* wqkv_blk = nullptr;
+  float* bqkv_blk = nullptr;
+  float* cqkv_blk = nullptr;
 };
 
 constexpr int kMaxT = 32;
@@ -316,6 +321,19 @@ int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH
     if (fold) {
       const std::vector<float> c = fold_ln(t, tb, g1, be1, 3 * D, D);
       if ((rc = upload_f32(h, c, &lw.cqkv))) return rc;
+      if (!qk_perm && (3 * D) % 256 == 0) {  // the row-blocked copy (LayerW::wqkv_blk)
+        const int64_t N3 = 3 * D;
+        std::vector<float> pt((size_t)N3 * D), pb(N3), pc(N3);
+        for (int64_t r = 0; r < N3; ++r) {
+          const int64_t w = r & 31, src = (r & ~31LL) + 8 * ((w >> 2) & 3) + 4 * (w >> 4) + (w & 3);
+          std::memcpy(pt.data() + (size_t)r * D, t.data() + (size_t)src * D, (size_t)D * 4);
+          pb[r] = tb[src];
+          pc[r] = c[src];
+        }
+        if ((rc = upload_mat(h, pt, &lw.wqkv_blk)) || (rc = upload_f32(h, pb, &lw.bqkv_blk)) ||
+            (rc = upload_f32(h, pc, &lw.cqkv_blk)))
+          return rc;
+      }
       if (qk_perm) {  // [q_h | k_h] per head (rows of the folded t, b', c)
         const int64_t DH = D / NH;
         std::vector<float> tq((size_t)2 * D * D), bq((size_t)2 * D), cq((size_t)2 * D);
@@ -556,6 +574,8 @@ struct Fwd {
     for (size_t li = 0; li < layers.size(); ++li) {
       LayerW& lw = layers[li];
       const bool last = li + 1 == layers.size();
+      // spatial layers: q|k|v in the row-blocked layout for the spatial attention kernel
+      const bool sblk = fold && xbf && lw.wqkv_blk && kind == ATT_VIDEO && S == 256 && fast_cap(cap) && !tattn;
       if (tattn) {
         // P (normalised bf16 probabilities, 512 B per (sequence, head)) goes to `big`; O to hb
         vp::EpiArgs ep;
@@ -575,6 +595,8 @@ struct Fwd {
           return gemm_bf16_w4(EPI_V_TATTN_LN, (const bf16_t*)xs, D, wv, D, M, D, D, ev, s); }));
       } else if (fold) {  // LN1 folded: A = the residual stream, (rstd, -mean*rstd) in ln_rs
         VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
+          if (sblk) return gemm(EPI_BF16_LN_BLK, xs, D, lw.wqkv_blk, 3 * D, big, 3 * D, lw.bqkv_blk, nullptr, nullptr, 1,
+                                nullptr, lw.cqkv_blk);
           return gemm(EPI_BF16_LN, xs, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr,
                       lw.cqkv); }));
       } else {
@@ -597,7 +619,7 @@ struct Fwd {
           if (S <= 256) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, cap, pad, s);
           return attention_masked(big, hb, 0, num_seq, S, NH, cap, pad, 0, s);
         }
-        if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, cap, pad, s);
+        if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, cap, pad, s, sblk);
         if (S <= 16) return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s);
         return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s); }));
       VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {

@@ -60,6 +60,9 @@ enum Epilogue {
   EPI_GELU_BF16_LN_BLK = 16,       // ffn_layer1 (as EPI_GELU_BF16_LN), h blocked
   EPI_RESID_FFN_BF16_ST_BLK = 17,  // ffn_layer2 (as EPI_RESID_FFN_BF16_ST), A = blocked h
   EPI_RESID_FFN_BF16_BLK = 18,     // ffn_layer2 (as EPI_RESID_FFN_BF16), A = blocked h
+  // the spatial layers' q|k|v projection (as EPI_BF16_LN) into the row-blocked layout [M/16][3D/32][16][32]
+  // (Wqkv / b' / c rows permuted the same way, a separate copy), read by attention_spatial_bf16(blk)
+  EPI_BF16_LN_BLK = 19,
 };
 
 struct EpiArgs {
@@ -115,8 +118,9 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
 // ---- attention (attention.hip) ----
 // qkv: rows of [q(D) | k(D) | v(D)], row r = seq * S + s; q pre-scaled by dh^-0.5.
 // o: rows of D = heads*64.  key_pad: optional [num_seq * S] (1 = padded key).
+// blk: qkv in the row-blocked layout of EPI_BF16_LN_BLK ([M/16][3D/32][16][32])
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
-                                  float cap, const float* key_pad, hipStream_t s);
+                                  float cap, const float* key_pad, hipStream_t s, bool blk = false);
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s);
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,

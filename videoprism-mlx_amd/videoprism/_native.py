@@ -141,6 +141,7 @@ _SIGNATURES = {
     "vp_dev_ln_stats": (c_int, [c_int, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "vp_dev_patch_embed": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
+    "vp_dev_attention_spatial_blk": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p, c_void_p]),
     "vp_dev_gemm_tattn": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_int64, c_float, c_void_p]),
 }
@@ -272,7 +273,7 @@ def dev_gemm_kernel(which, a, w, bias, epilogue, out, resid=None, pos=None, rowp
 
 EPI_BF16_LN, EPI_GELU_LN, EPI_RESID_BF16_ST, EPI_RESID_FFN_BF16_ST, EPI_POS_BF16_ST = 8, 9, 10, 11, 12
 # the FFN pair over the row-blocked hidden activation [M/16][F/32][16][32] (vp_kernels.h EPI_*_BLK)
-EPI_GELU_LN_BLK, EPI_RESID_FFN_BF16_ST_BLK, EPI_RESID_FFN_BF16_BLK = 16, 17, 18
+EPI_GELU_LN_BLK, EPI_RESID_FFN_BF16_ST_BLK, EPI_RESID_FFN_BF16_BLK, EPI_BF16_LN_BLK = 16, 17, 18, 19
 
 
 def ffn1_blk_rows(F):
