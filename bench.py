@@ -84,11 +84,11 @@ WORKLOADS = {
 }
 
 
-def cpu_baseline(cfg, variables, runs: int = 3) -> dict:
+def cpu_baseline(cfg, variables, runs: int = 5, warmups: int = 2) -> dict:
     """Oracle (NumPy fp32, TEST INFRASTRUCTURE) on one clip -- a reported baseline only.  BLAS
-    threads pinned to CPU_BASELINE_THREADS (the box's CPU share per GPU); one untimed warm-up
-    run, then `runs` timed runs: value = 1 / mean, with mean +- std in the sample text
-    (SURVEY §8(d) method, scaled to the bench's time budget)."""
+    threads pinned to CPU_BASELINE_THREADS (the box's CPU share per GPU); `warmups` untimed runs,
+    then `runs` timed runs: value = 1 / mean, with mean +- std in the sample text (SURVEY §8(d):
+    B = 1, warm-up 2, runs 5, mean +- std; about 30 s of CPU work)."""
     import numpy as np
     from threadpoolctl import threadpool_info, threadpool_limits
 
@@ -98,17 +98,17 @@ def cpu_baseline(cfg, variables, runs: int = 3) -> dict:
     times = []
     with threadpool_limits(limits=CPU_BASELINE_THREADS):
         threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-        for i in range(runs + 1):
+        for i in range(runs + warmups):
             t0 = time.perf_counter()
             orc.factorized_encoder(variables["params"], video, cfg, mode="f32")
-            if i > 0:
+            if i >= warmups:
                 times.append(time.perf_counter() - t0)
     mean, std = float(np.mean(times)), float(np.std(times))
     return {"value": round(1.0 / mean, 5), "unit": "clips/s", "cores": int(threads), "kind": "port",
             "blas_threads": int(threads), "host_cpus_schedulable": len(os.sched_getaffinity(0)),
             "host_cpus_total": os.cpu_count(),
             "sample": f"1 clip [1,16,288,288,3], full {cfg.get('_name', 'model')} forward, NumPy fp32 "
-                      f"oracle (oracle/videoprism_oracle.py): 1 warm-up + {runs} timed runs, "
+                      f"oracle (oracle/videoprism_oracle.py): {warmups} warm-up + {runs} timed runs, "
                       f"{mean:.2f} +- {std:.2f} s per clip (min {min(times):.2f}, max {max(times):.2f}) "
                       f"with BLAS pinned to {threads} threads; the host exposes "
                       f"{len(os.sched_getaffinity(0))} schedulable CPUs.  For context, the reference's "
