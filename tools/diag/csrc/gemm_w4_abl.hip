@@ -32,18 +32,4 @@ hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf1
   return hipErrorInvalidValue;
 }
 
-// the LN-folded epilogues (which 0: EPI_BF16_LN q|k|v, S3; 1: EPI_GELU_BF16_LN ffn_layer1, no padded
-// rows) with ABL bits (16: row statistics not loaded; 32: next tile's statistics requested at the epilogue)
-hipError_t gemm_bf16_w4_ln_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
-                               const EpiArgs& ep, hipStream_t s) {
-  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
-  if (which == 0 && abl == 0) return launch_w4<EPI_BF16_LN, false, true, 0>(A, K, W, K, M, N, K, ep, s);
-  if (which == 0 && abl == 16) return launch_w4<EPI_BF16_LN, false, true, 16>(A, K, W, K, M, N, K, ep, s);
-  if (which == 1 && abl == 0) return launch_w4<EPI_GELU_BF16_LN, true, false, 0>(A, K, W, K, M, N, K, ep, s);
-  if (which == 1 && abl == 16) return launch_w4<EPI_GELU_BF16_LN, true, false, 16>(A, K, W, K, M, N, K, ep, s);
-  if (which == 0 && abl == 32) return launch_w4<EPI_BF16_LN, false, true, 32>(A, K, W, K, M, N, K, ep, s);
-  if (which == 1 && abl == 32) return launch_w4<EPI_GELU_BF16_LN, true, false, 32>(A, K, W, K, M, N, K, ep, s);
-  return hipErrorInvalidValue;
-}
-
 }  // namespace vp

@@ -20,8 +20,6 @@ hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const
                             int N, int K, const EpiArgs& ep, hipStream_t s);
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
                                   const EpiArgs& ep, hipStream_t s);
-hipError_t gemm_bf16_w4_ln_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
-                               const EpiArgs& ep, hipStream_t s);
 // q|k|v projection (LN1 folded, EPI_BF16_LN arithmetic) + spatial attention (S = 256, dh = 64,
 // D = 768, no key paddings) fused per (frame, head) (qkv_attention.hip); bitwise equal to
 // gemm_bf16_w4(EPI_BF16_LN) followed by attention_spatial_bf16.

@@ -37,19 +37,6 @@ int vp_dev_gemm_tattn_abl(int which, int abl, const void* A, const void* W, int6
   return VP_OK;
 }
 
-// the LN-folded GEMMs with ablation bits (which 0: q|k|v EPI_BF16_LN, 1: ffn_layer1 EPI_GELU_BF16_LN)
-int vp_dev_gemm_ln_abl(int which, int abl, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
-                       const float* bias, const float* ln_rs, const float* ln_c, void* stream) {
-  using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
-  if (e) return fail(VP_EINVAL, e);
-  EpiArgs ep;
-  ep.out = out; ep.ldo = N; ep.bias = bias; ep.ln_rs = ln_rs; ep.ln_c = ln_c; ep.cap = 1.0f;
-  VP_HIP(gemm_bf16_w4_ln_abl(which, abl, (const bf16_t*)A, (const bf16_t*)W, (int)M, (int)N, (int)K, ep,
-                             static_cast<hipStream_t>(stream)));
-  return VP_OK;
-}
-
 // the overlapped-epilogue GEMM (gemm_bf16_ov.hip) with the plain bf16-output epilogues
 int vp_dev_gemm_ov(int epi, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
                    const float* bias, const void* resid, void* stream) {

@@ -204,40 +204,11 @@ def tattn(dev, g):
     print("tattn:", " | ".join(f"{k} {min(v)*1e3:7.1f} us" for k, v in res.items()), flush=True)
 
 
-def lnrs(dev, g):
-    """The LN-folded GEMMs (q|k|v, ffn_layer1 at the bench shape) against their builds that skip the
-    tile-start row-statistics loads (diag ABL 16): what those loads cost at the head of every tile's
-    vmcnt queue; and the build that requests the next tile's rows at the epilogue's start (ABL 32).
-    Interleaved rounds."""
-    for which, name, N in ((0, "qkv", 2304), (1, "ffn1", 3072)):
-        M, K = M_TOK, 768
-        a, w, b = operands(M, N, K, g, dev)
-        c = torch.zeros(N, device=dev)
-        rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
-        o = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        st = lambda: torch.cuda.current_stream().cuda_stream
-        run = lambda abl: nat.call("vp_dev_gemm_ln_abl", which, abl, a.data_ptr(), w.data_ptr(), M, N, K, o.data_ptr(),
-                                   b.data_ptr(), rs.data_ptr(), c.data_ptr(), st())
-        outs = {}
-        for k in (0, 32):
-            run(k)
-            torch.cuda.synchronize()
-            outs[k] = o.clone()
-        res = {k: [] for k in (0, 16, 32)}
-        for _ in range(4):
-            for k in res:
-                res[k].append(timeit(lambda: run(k)))
-        print(f"{name}: with row statistics {min(res[0])*1e3:7.1f} us | without {min(res[16])*1e3:7.1f} us | "
-              f"next tile's requested at the epilogue {min(res[32])*1e3:7.1f} us (bitwise {torch.equal(outs[0], outs[32])})",
-              flush=True)
-        del a, o
-
-
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn, "lnrs": lnrs}
+    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn}
     modes.get(mode, compare)(dev, g)
 
 

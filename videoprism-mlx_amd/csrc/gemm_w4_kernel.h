@@ -88,9 +88,7 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 // ABL: ablation builds for the tools' diag library only (tools/diag/csrc/gemm_w4_abl.hip; results
 // are garbage; the product library instantiates ABL = 0 only): 2 = no ds_reads in the K-loop,
 // 4 = no staging loads after the prologue, 8 = no epilogue (stores skipped at run time; the
-// accumulators stay live); 16 = the LN-folded epilogues' row statistics not loaded (prices their
-// place at the head of each tile's vmcnt queue); 32 = the next tile's row statistics requested at the
-// start of this tile's epilogue (bitwise equal).
+// accumulators stay live).
 
 // the LN fold of 4 accumulator values (r * a + (m * c + b)) in packed pairs: two IEEE fmas per value
 // (the scalar form is bitwise equal and measured no faster beside the fused epilogues' MFMAs:
@@ -338,22 +336,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
 
   int g = 0;
   const int er = lane >> 3, es = lane & 7;  // epilogue read-back: row pass*8 + er, column segment es
-  // RSPF (EPI_*_LN): the row statistics of tile j+1 are requested at the start of tile j's epilogue,
-  // where they queue behind nothing the epilogue waits for, instead of at tile j+1's start, where they
-  // sit ahead of its K-stream in the vmcnt queue
-  constexpr bool kRsPf = EpiTraits<EPI>::kLn && (ABL & 32) != 0;
-  float2 rsn[8][2];
-  auto ld_rs_tile = [&](int jt) {
-    int ttm, ttn;
-    coords(first + jt * stride, ttm, ttn);
-    const int mb = ttm * BM + wm * 128 + er;
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt)
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass)
-        rsn[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
-  };
-  if constexpr (kRsPf) ld_rs_tile(0);
   for (int j = 0; j < count; ++j) {
     // this tile's bias columns, requested before any of the tile's K-stream loads: vmcnt
     // retires in issue order, so a bias load issued in the epilogue would wait for the next
@@ -391,9 +373,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
           for (int pass = 0; pass < 2; ++pass)
-            rs[mt][pass] = kRsPf ? rsn[mt][pass]
-                                 : (ABL & 16) ? make_float2(ep.cap, ep.cap_c1)
-                                              : *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
+            rs[mt][pass] = *reinterpret_cast<const float2*>(ep.ln_rs + 2 * (int64_t)(mb + mt * 16 + pass * 8));
       }
     }
     if constexpr (EpiTraits<EPI>::kVAttn || EpiTraits<EPI>::kQkAttn) {  // last K-tile peeled (K >= 2 BK)
@@ -657,9 +637,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-    }
-    if constexpr (kRsPf) {
-      if (j + 1 < count) ld_rs_tile(j + 1);
     }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)

@@ -153,8 +153,6 @@ _DIAG_SIGNATURES = {
     "vp_dev_attention_long_var": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_tattn_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
-    "vp_dev_gemm_ln_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
-                                   c_void_p, c_void_p, c_void_p, c_void_p]),
     "vp_dev_gemm_w4_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                    c_void_p, c_void_p]),
     "vp_dev_gemm_ov": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
