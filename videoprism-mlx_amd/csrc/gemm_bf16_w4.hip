@@ -32,6 +32,9 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
   // (x in the Infinity Cache for the next GEMM) and on the q|k|v projection (for the spatial attention)
   // measured no faster.
   constexpr bool S3 = true, S2 = false;
+  // the S3 residual epilogues peel their last K-tile (gemm_w4_kernel.h kEarly: K >= 2 BK); the
+  // other bf16-residual epilogues take S3 only for K >= 2048
+  if (K < 2 * BK && epi == EPI_RESID_BF16_ST) return hipErrorInvalidValue;
   switch (epi) {
     case EPI_BF16: return launch_w4<EPI_BF16, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_GELU_BF16: return launch_w4<EPI_GELU_BF16, false, S2>(A, lda, W, ldw, M, N, K, ep, s);

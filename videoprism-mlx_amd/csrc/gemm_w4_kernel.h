@@ -293,11 +293,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // h1 of K-tile g (buffer cb): MFMAs set 1, reads of set 0 <- (g+1, h0) from buffer cb^1,
   // 16 loads of K-tile g+2 into buffer cb.  DEFER (the fused temporal launches' last K-tile of a
   // tile): the reads of set 0 are left to the end of the epilogue, so their 64 registers are free in it
-  auto h1 = [&](int cb, auto DEFER) {
+  // EARLY (kEarly's last K-tile): 4 residual loads were issued after this K-tile's h0 pieces
+  auto h1 = [&](int cb, auto DEFER, auto EARLY) {
     constexpr bool defer = decltype(DEFER)::value;
+    constexpr bool early = decltype(EARLY)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // S3: K-tile g+1 has landed once all but this K-tile's h0 A pieces (of g+2) are done
-    if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (S3 && early) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sched_fence();
     mfma(1, 0, false);
@@ -344,10 +347,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     float4 cl[2], ch[2];  // EPI_*_LN: column sums of W'
     float2 rs[8][2];      // EPI_*_LN: (rstd, -mean*rstd) of rows mt*16 + pass*8 + er
     float2 rsb[8];        // EPI_GELU_BF16_LN_BLK: (rstd, -mean*rstd) of rows mt*16 + (lane & 15)
+    // S3 epilogues with a bf16 residual (post, ffn_layer2): the residual rows of the first row block are
+    // requested inside the tile's last K-tile (after its h0 staging loads, so h1's vmcnt(8) still
+    // names that K-tile's pieces) and kept raw until the epilogue uses them -- their memory latency
+    // overlaps the last K-tile's MFMAs instead of opening the epilogue
+    constexpr bool kEarly = EpiTraits<EPI>::kResidBf16 && S3;
+    uint4 exr[2][2][2];   // kEarly: raw residual [buffer][nh][pass]
+    int m0t = 0, n0t = 0;  // kEarly: this tile's wave origin (the epilogue's m0, n0)
     float keepb[8];       // EPI_GELU_BF16_LN_BLK with padded rows: 1 - rowpad of the same rows
     {
       int ttm, ttn;
       coords(first + j * stride, ttm, ttn);
+      m0t = ttm * BM + wm * 128;
+      n0t = ttn * BN + wn * 128;
       const int nb = ttn * BN + wn * 128 + es * 8;
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) {
@@ -378,22 +390,42 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     if constexpr (EpiTraits<EPI>::kVAttn || EpiTraits<EPI>::kQkAttn) {  // last K-tile peeled (K >= 2 BK)
       h0(g & 1, true);
-      h1(g & 1, std::false_type{});
+      h1(g & 1, std::false_type{}, std::false_type{});
       ++g;
       for (int kt = 1; kt < nk - 1; ++kt, ++g) {
         h0(g & 1, false);
-        h1(g & 1, std::false_type{});
+        h1(g & 1, std::false_type{}, std::false_type{});
       }
       h0(g & 1, false);
-      h1(g & 1, std::true_type{});
+      h1(g & 1, std::true_type{}, std::false_type{});
       ++g;
     } else {
+      auto fetch_raw = [&](int bsel, int mt) {
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int pass = 0; pass < 2; ++pass)
+            exr[bsel][nh][pass] = *reinterpret_cast<const uint4*>(
+                static_cast<const bf16_t*>(ep.resid) + (int64_t)(m0t + mt * 16 + pass * 8 + er) * ep.ldr + n0t +
+                nh * 64 + es * 8);
+      };
       h0(g & 1, true);
-      h1(g & 1, std::false_type{});
+      h1(g & 1, std::false_type{}, std::false_type{});
       ++g;
-      for (int kt = 1; kt < nk; ++kt, ++g) {
+      if constexpr (kEarly) {  // last K-tile peeled (the launcher checks K >= 2 BK)
+        for (int kt = 1; kt < nk - 1; ++kt, ++g) {
+          h0(g & 1, false);
+          h1(g & 1, std::false_type{}, std::false_type{});
+        }
         h0(g & 1, false);
-        h1(g & 1, std::false_type{});
+        fetch_raw(0, 0);
+        h1(g & 1, std::false_type{}, std::true_type{});
+        ++g;
+      } else {
+        for (int kt = 1; kt < nk; ++kt, ++g) {
+          h0(g & 1, false);
+          h1(g & 1, std::false_type{}, std::false_type{});
+        }
       }
     }
 
@@ -640,13 +672,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     // residual / position rows of block mt+1 are requested before block mt's stores, so a
     // load never waits behind the stores just issued (vmcnt retires in issue order)
-    F8 ex[2][2][2];  // [buffer][nh][pass]
+    F8 ex[2][2][2];  // [buffer][nh][pass] (kEarly: exr, raw)
     auto fetch = [&](int bsel, int mt) {
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-        for (int pass = 0; pass < 2; ++pass)
-          ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+        for (int pass = 0; pass < 2; ++pass) {
+          if constexpr (kEarly)
+            exr[bsel][nh][pass] = *reinterpret_cast<const uint4*>(
+                static_cast<const bf16_t*>(ep.resid) + (int64_t)(m0 + mt * 16 + pass * 8 + er) * ep.ldr + n0 + nh * 64 +
+                es * 8);
+          else
+            ex[bsel][nh][pass] = epi_extra8<EPI>(ep, m0 + mt * 16 + pass * 8 + er, n0 + nh * 64 + es * 8, N);
+        }
     };
     // block G = (mt, nh): acc[nh*4 + q][mt], q = 0..3 -> scratch buffer G & 1.  Block G+1 is
     // written before block G is read back, so the LDS round trip overlaps the math and stores.
@@ -663,7 +701,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     // es keeps the partials of mt == es, so the wave stores its 128 rows with 2 instructions
     float sv[2][8];
     float pS[2] = {0.f, 0.f}, pQ[2] = {0.f, 0.f};
-    if constexpr (Tr::kExtra) fetch(0, 0);
+    if constexpr (Tr::kExtra && !kEarly) fetch(0, 0);
     put(0);
 #pragma unroll
     for (int G = 0; G < 16; ++G) {
@@ -703,7 +741,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
           if (ep.rowpad) keep = 1.0f - ep.rowpad[row];
         }
         {
-          const epi_u32x4 pk = epi_store8<EPI, !Tr::kResidStream, !NOPAD>(ep, row, n, v, keep, ex[mt & 1][nh][pass]);
+          F8 e;
+          if constexpr (kEarly) {  // the same conversion as epi_extra8
+            const uint4 u = exr[mt & 1][nh][pass];
+            e.lo = bf16x4_to_f32(make_uint2(u.x, u.y));
+            e.hi = bf16x4_to_f32(make_uint2(u.z, u.w));
+          } else {
+            e = ex[mt & 1][nh][pass];
+          }
+          const epi_u32x4 pk = epi_store8<EPI, !Tr::kResidStream, !NOPAD>(ep, row, n, v, keep, e);
           if constexpr (Tr::kStats) {
             float y[8];
 #pragma unroll
