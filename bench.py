@@ -141,6 +141,17 @@ def _free_port() -> int:
     return p
 
 
+def rank_env(rank: int, world: int, port: int, base=None) -> dict:
+    """A spawned rank's environment: the launcher variables, plus HSA_ENABLE_IPC_MODE_LEGACY=0
+    when the caller left it unset (the host driver supports dmabuf IPC only; without it RCCL's
+    peer setup fails with 'hipIpcGetMemHandle: invalid argument').  The parent has not touched
+    the GPU, so this is a fresh child's environment, not a re-exec.  An explicit value is kept."""
+    env = dict(os.environ if base is None else base, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
 def spawn_ranks(n: int, timeout_s: float) -> int:
     """--gpus N without a launcher: N child processes of this script (RANK/LOCAL_RANK/WORLD_SIZE/
     MASTER_ADDR/MASTER_PORT set), started before this parent touches any GPU.  All children are
@@ -150,9 +161,8 @@ def spawn_ranks(n: int, timeout_s: float) -> int:
     port = _free_port()
     procs = []
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=rank_env(r, n, port)))
     deadline = time.monotonic() + timeout_s
     rc = 0
     while True:
@@ -445,7 +455,8 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
         standin_check = {"gathered_shape": list(rows.shape) if rows is not None else None,
                          "row_order_ok": bool(rows is not None and rows.shape == ref.shape and
                                               torch.allclose(rows, ref, atol=1e-6)),
-                         "similarity_shape": list(last["sim"].shape) if "sim" in last else None}
+                         "similarity_shape": list(last["sim"].shape) if "sim" in last else None,
+                         "ipc_mode_legacy": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")}
 
     if rank == 0:
         label = {"base": "VideoPrism-Base fwd", "large": "VideoPrism-Large fwd",

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define VP_ABI_VERSION 4
+#define VP_ABI_VERSION 5
 
 typedef struct vp_handle vp_handle;
 
@@ -93,6 +93,12 @@ int vp_finalize(vp_handle* h);
  * 'bilinear', antialiased when shrinking) and caches it on the device (allocates; call once per
  * new frame size before vp_forward, which never allocates). */
 int vp_prepare_geometry(vp_handle* h, int64_t H, int64_t W);
+
+/* Clips of T frames: the temporal positional table resampled to T the way encoders.py:543-553
+ * does (_interpolate_emb_1d, :107-130, jax.image.resize 'bilinear', antialiased when shrinking).
+ * vp_finalize precomputes T = 1..32; any other T needs one call before vp_forward (allocates;
+ * idempotent).  1 <= T <= 2^20. */
+int vp_prepare_frames(vp_handle* h, int64_t T);
 
 /* Workspace needed by vp_forward for inputs [B, T, H, W, 3]. */
 int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W,

@@ -151,6 +151,25 @@ def dot_atten(q, k, v, mask, nm: Numerics, cap: float, dim_per_head: int):
     q,k,v: [B, S, N, H]; mask: [B|1, 1, 1, S] (or None for all-valid).
     """
     q = nm.act(q * nm.act(dim_per_head ** -0.5))          # per_dim_scale disabled
+    B, T, N, _ = q.shape
+    S = k.shape[1]
+    qc = max(1, _ATTN_CHUNK_ELEMS // max(1, B * N * S))
+    if qc < T:
+        # every query row's softmax is independent of the others: long sequences (the LvT
+        # auxiliary encoder at T*N = 10240 tokens) run in query blocks so the [B, N, T, S]
+        # logits never exist at once -- the same elementwise operations per row
+        def rows(m, i):
+            return m if m is None or m.shape[-2] == 1 else m[..., i:i + qc, :]
+        return np.concatenate([_dot_atten_rows(q[:, i:i + qc], k, v, rows(mask, i), nm, cap)
+                               for i in range(0, T, qc)], axis=1)
+    return _dot_atten_rows(q, k, v, mask, nm, cap)
+
+
+_ATTN_CHUNK_ELEMS = 1 << 27   # logits elements per query block (1 GiB in fp64)
+
+
+def _dot_atten_rows(q, k, v, mask, nm: Numerics, cap: float):
+    """dot_atten's body after _scale_query, for a block of (already scaled) query rows."""
     qt = np.transpose(q, (0, 2, 1, 3))                      # B N T H
     kt = np.transpose(k, (0, 2, 3, 1))                      # B N H S
     logits = nm.act(np.matmul(qt, kt))                      # 'BTNH,BSNH->BNTS'

@@ -110,19 +110,28 @@ def full_video(seed, T=16):
     return np.random.default_rng(seed).random((1, T, 288, 288, 3), dtype=np.float32)
 
 
-def g_full(tag):
+def g_full(tag, T=16, modes=("f64", "bf16")):
     name, pseed, vseed = FULL[tag]
     cfg = models.CONFIGS[name]
     var = params.synthetic_params(cfg, seed=pseed)
-    x = full_video(vseed)
-    arrays = dict(param_seed=np.array(pseed), video_seed=np.array(vseed), model=np.array(name))
-    for mode in ("f64", "bf16"):
+    x = full_video(vseed, T)
+    arrays = dict(param_seed=np.array(pseed), video_seed=np.array(vseed), model=np.array(name), T=np.array(T))
+    for mode in modes:
         e, _ = orc.factorized_encoder(var["params"], x, cfg, mode)
         m = e.astype(np.float64).mean(axis=1)
         arrays[f"pooled_{mode}"] = m / np.sqrt((m * m).sum(-1, keepdims=True) + 1e-12)
-        arrays[f"rows_{mode}"] = e[0, ::64].astype(np.float32)
-        arrays[f"frame_mean_{mode}"] = e[0].reshape(16, -1, e.shape[-1]).mean(axis=1).astype(np.float32)
+        # fp64 rows for the fp32 bar (1e-5); float32 storage would round them by up to ~1e-7 * |y|
+        arrays[f"rows_{mode}"] = e[0, ::64].astype(np.float64 if T > 16 else np.float32)
+        arrays[f"frame_mean_{mode}"] = e[0].reshape(T, -1, e.shape[-1]).mean(axis=1).astype(np.float32)
     np.savez_compressed(os.path.join(HERE, f"{tag}.npz"), **arrays)
+
+
+# Clips longer than the temporal table (encoders.py:543-553 interpolates the
+# temporal pos-emb to any T): full-depth Base at T = 48 / 64 (16 -> 48 / 64) and Large at T = 48
+# (8 -> 48), fp64 only (the bf16 bars are the pooled vector and the token mean-abs)
+LONG = {"g9_base_t48": ("videoprism_v1_base", 0, 21, 48), "g10_base_t64": ("videoprism_v1_base", 0, 22, 64),
+        "g11_large_t48": ("videoprism_v1_large", 0, 23, 48)}
+FULL.update({k: v[:3] for k, v in LONG.items()})
 
 
 # configs[4]'s per-rank workload at full depth: FactorizedVideoCLIP with videoprism_lvt_v1_large
@@ -161,8 +170,31 @@ def g8_lvt_large_t16():
     np.savez_compressed(os.path.join(HERE, "g8_lvt_large_t16.npz"), **arrays)
 
 
+# LvT-Base at T = 40 (SURVEY §8(f) f1 + f3): the full-depth FactorizedVideoCLIP whose auxiliary
+# encoder attends over T*N = 10240 tokens per clip (encoders.py:846-857); fp64 video / text
+# embeddings, similarity and frame embeddings.
+G12 = dict(cfg="videoprism_lvt_v1_base", vocabulary_size=32000, param_seed=12, video_seed=32, text_seed=42,
+           Q=2, L=64, T=40)
+
+
+def g12_lvt_base_t40():
+    cfg = dict(models.CONFIGS[G12["cfg"]])
+    cfg["vocabulary_size"] = G12["vocabulary_size"]
+    var = params.synthetic_params(cfg, seed=G12["param_seed"], specs=params.clip_leaf_specs(cfg))
+    x = full_video(G12["video_seed"], G12["T"])
+    ids, pads = g8_text(G12["text_seed"], G12["Q"], G12["L"], cfg["vocabulary_size"])
+    arrays = {k: np.array(v) for k, v in G12.items()}
+    arrays.update(text_token_ids=ids, text_paddings=pads)
+    v, t, out = orc.video_clip(var["params"], cfg, x, ids, pads, "f64", return_intermediate=("frame_embeddings",))
+    arrays["video_emb_f64"] = np.asarray(v, np.float64)
+    arrays["text_emb_f64"] = np.asarray(t, np.float64)
+    arrays["similarity_f64"] = np.asarray(v, np.float64) @ np.asarray(t, np.float64).T
+    arrays["frame_emb_f64"] = np.asarray(out["frame_embeddings"], np.float64)
+    np.savez_compressed(os.path.join(HERE, "g12_lvt_base_t40.npz"), **arrays)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8"]
+    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12"]
     if "g1" in which:
         g1_tiny()
     if "g2" in which:
@@ -172,10 +204,15 @@ if __name__ == "__main__":
     if "g5" in which:
         g5_clip_tiny()
     for tag in FULL:
-        if tag[:2] in which:
-            g_full(tag)
+        if tag.split("_")[0] in which:
+            if tag in LONG:
+                g_full(tag, T=LONG[tag][3], modes=("f64",))
+            else:
+                g_full(tag)
     if "g8" in which:
         g8_lvt_large_t16()
+    if "g12" in which:
+        g12_lvt_base_t40()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

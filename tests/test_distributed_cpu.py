@@ -75,12 +75,17 @@ def _bench_env():
                                                              "MASTER_ADDR", "MASTER_PORT")}
 
 
-def _bench_standin(workload, batch):
+def _bench_standin(workload, batch, env_update=None):
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = _bench_env()
+    for k, v in (env_update or {}).items():
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--standin",
                         "--workload", workload, "--batch", str(batch), "--frames", "2", "--steps", "2",
                         "--warmup", "1"], capture_output=True, text=True, timeout=150, env=env)
@@ -94,10 +99,25 @@ def _bench_standin(workload, batch):
 def test_bench_spawns_world2_base_gather():
     """`bench.py --gpus 2` without a launcher spawns 2 ranks and drives its real step logic (pool ->
     gather) with the CPU stand-in forward: rank-major rows of all 2*b clips, n_gpus == 2."""
-    line = _bench_standin("base", 2)
+    line = _bench_standin("base", 2, {"HSA_ENABLE_IPC_MODE_LEGACY": None})
     assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 4
     chk = line["standin_check"]
     assert chk["gathered_shape"] == [4, 768] and chk["row_order_ok"]
+    # the parent had HSA_ENABLE_IPC_MODE_LEGACY unset: the spawned ranks get 0 (dmabuf IPC)
+    assert chk["ipc_mode_legacy"] == "0"
+
+
+def test_rank_env_keeps_an_explicit_ipc_mode():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    env = bench.rank_env(1, 4, 29500, base={"PATH": "/bin"})
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"]) == ("1", "1", "4")
+    assert (env["MASTER_ADDR"], env["MASTER_PORT"]) == ("127.0.0.1", "29500")
+    assert bench.rank_env(0, 2, 1, base={"HSA_ENABLE_IPC_MODE_LEGACY": "1"})["HSA_ENABLE_IPC_MODE_LEGACY"] == "1"
 
 
 @pytest.mark.timeout(200)

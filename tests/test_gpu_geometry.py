@@ -48,3 +48,61 @@ def test_geometry_bf16(cuda, H, T):
     pool_err = np.abs(_pooled(emb) - _pooled(ref)).max()
     print(f"bf16 H={H} T={T}: token mean-abs {mean_err:.3e} pooled {pool_err:.3e}")
     assert mean_err < 2e-2 and pool_err < 1e-3
+
+
+@pytest.mark.parametrize("P", [16, 9])
+def test_other_patch_sizes_bf16(cuda, P):
+    """Patch sizes other than 18 on the 16 x 16 grid (H = 16 P): even P takes the fused patch
+    embedding straight from the frames, odd P (16-B chunks only 2-B aligned) patchify + GEMM
+    (vp_kernels.h video_patch_ok).  Base dims, 1+1 layers, vs the oracle fp64."""
+    cfg = dict(models.CONFIGS["videoprism_v1_base"])
+    cfg.update(num_spatial_layers=1, num_temporal_layers=1, patch_size=P)
+    var = params.synthetic_params(cfg, seed=P)
+    video = np.random.default_rng(P).random((2, 4, 16 * P, 16 * P, 3), dtype=np.float32)
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedEncoder(**cfg), fprop_dtype=torch.bfloat16)
+    emb, _ = m.apply(var, video)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, "f64")
+    emb = np.asarray(emb, np.float64)
+    mean_err = np.abs(emb - ref).mean()
+    pool_err = np.abs(_pooled(emb) - _pooled(ref)).max()
+    print(f"bf16 P={P}: token mean-abs {mean_err:.3e} pooled {pool_err:.3e}")
+    assert mean_err < 2e-2 and pool_err < 1e-3
+
+
+def test_misaligned_frames_take_the_patchify_path(cuda):
+    """Frames at an address the fused path's chunk reads (4 B) or video_to_bf16's vector loads
+    (16 B for fp32, 4 B for uint8) do not meet -- a view into a larger buffer, handed to the engine
+    as it is (apply() would cast fp32 frames to a fresh, aligned bf16 tensor) -- run patchify +
+    GEMM: bf16 / fp32 / uint8 views at odd offsets give bitwise the same result as each other
+    (the fp32 values are IEEE u8 / 255, the kernel's own conversion), within the pooled bar of
+    the oracle and within bf16 rounding of the aligned (fused) forward."""
+    cfg = dict(models.CONFIGS["videoprism_v1_base"])
+    cfg.update(num_spatial_layers=1, num_temporal_layers=1)
+    var = params.synthetic_params(cfg, seed=31)
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedEncoder(**cfg), fprop_dtype=torch.bfloat16)
+    eng = m.engine(var, torch.cuda.current_device())
+    shape = (1, 2, 288, 288, 3)
+    n = int(np.prod(shape))
+    u8n = np.random.default_rng(31).integers(0, 256, n, dtype=np.uint8)
+    f32n = u8n.astype(np.float32) / np.float32(255.0)
+    u8 = torch.from_numpy(u8n).to(cuda)
+    f32 = torch.from_numpy(f32n).to(cuda)
+    bf = f32.to(torch.bfloat16)
+    outs = {}
+    for name, flat in (("bf16", bf), ("f32", f32), ("u8", u8)):
+        buf = torch.zeros(n + 1, dtype=flat.dtype, device=cuda)
+        buf[1:] = flat
+        view = buf[1:].view(shape)
+        assert view.is_contiguous() and view.data_ptr() % (16 if flat.dtype == torch.float32 else 4) != 0
+        outs[name] = eng.forward(view)[0].clone()
+    aligned = eng.forward(bf.view(shape).contiguous())[0]
+    torch.cuda.synchronize()
+    assert torch.equal(outs["bf16"], outs["f32"]) and torch.equal(outs["bf16"], outs["u8"])
+    ref, _ = orc.factorized_encoder(var["params"], f32n.reshape(shape), cfg, "f64")
+    got = outs["bf16"].double().cpu().numpy()
+    pool_err = np.abs(_pooled(got) - _pooled(ref)).max()
+    d = (outs["bf16"].double() - aligned.double()).abs()
+    print(f"misaligned frames: pooled {pool_err:.3e} vs oracle; vs the aligned fused forward max {float(d.max()):.3e} "
+          f"mean {float(d.mean()):.3e}")
+    assert pool_err < 1e-3
+    assert float(d.mean()) < 2e-3

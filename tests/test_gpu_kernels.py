@@ -567,14 +567,16 @@ def test_temporal_attention_fused_kernels_vs_unfused(cuda, heads):
         assert bool(((o - ref).abs() <= 2 ** -7 * ref.abs() + 2 ** -7 * vmax).all())
 
 
-@pytest.mark.parametrize("frames", [3, 9])
-def test_patch_embed_fused_from_frames(cuda, frames):
+@pytest.mark.parametrize("frames,P", [(3, 18), (9, 18), (3, 16), (3, 14), (4, 10), (5, 4)])
+def test_patch_embed_fused_from_frames(cuda, frames, P):
     """The fused patch embedding (gemm_bf16_w4_video: the GEMM stages its A tiles straight from the
     bf16 frames in 16-B chunks of the patch pixel rows, no patch tensor) against the two-kernel
     path (patchify -> [M, 1024] patches -> GEMM) and against fp64 on the same bf16 frames: the sums
     differ only in their fp32 order (at most one bf16 ulp apart), and the fused result is within one
-    bf16 rounding of fp64.  The chunk that overlaps its predecessor must meet zero weights there."""
-    P, D = 18, 768
+    bf16 rounding of fp64.  The chunk that overlaps its predecessor must meet zero weights there.
+    Every even P the fused path takes (vp_kernels.h video_patch_ok): 3P = 54, 48, 42, 30, 12 values
+    per pixel row, i.e. 7 / 6 / 6 / 4 / 2 chunks with and without an overlapping last chunk."""
+    D = 768
     g = torch.Generator(device="cpu").manual_seed(frames)
     v = _bf(torch.rand(frames, 16 * P, 16 * P, 3, generator=g) * 4 - 1)
     k = torch.randn(P * P * 3, D, generator=g) / (P * P * 3) ** 0.5
@@ -597,5 +599,16 @@ def test_patch_embed_fused_from_frames(cuda, frames):
     # a power of two); each within half an ulp of fp64 plus the fp32 summation error
     assert np.all(np.abs(f - t) <= 2 ** -7 * np.abs(ref) + 1e-5), np.abs(f - t).max()
     assert np.all(np.abs(f - ref) <= 2 ** -8 * np.abs(ref) + 1e-4), np.abs(f - ref).max()
-    print(f"fused patch embedding, {frames} frames: vs two-kernel max {np.abs(f - t).max():.3e} "
+    print(f"fused patch embedding P={P}, {frames} frames: vs two-kernel max {np.abs(f - t).max():.3e} "
           f"(mean {np.abs(f - t).mean():.2e}); vs fp64 max {np.abs(f - ref).max():.3e}")
+
+
+def test_patch_embed_fused_rejects_odd_patch(cuda):
+    """Odd P would put the 16-B chunks at 2-B offsets in the frame: the fused launcher refuses them
+    (the encoder takes patchify + GEMM for such grids, test_gpu_geometry.py)."""
+    P, D = 9, 768
+    v = torch.zeros(1, 16 * P, 16 * P, 3, device=cuda, dtype=torch.bfloat16)
+    wv = torch.zeros(D, 64 * P, device=cuda, dtype=torch.bfloat16)
+    out = torch.empty(256, D, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="even patch size"):
+        nat.dev_patch_embed(v, P, wv, torch.zeros(D, device=cuda), torch.zeros(256, D, device=cuda), out)

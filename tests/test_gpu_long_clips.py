@@ -1,0 +1,199 @@
+"""Clips longer than 32 frames.  The reference accepts any T: the temporal
+positional table is resampled to T (encoders.py:543-553 -> _interpolate_emb_1d :107-130,
+jax.image.resize 'bilinear'), and the temporal encoder is a length-T sequence (:556-566).  Here
+vp_finalize precomputes the tables for T = 1..32 and vp_prepare_frames makes any other one on
+first sight (the Python engines call it, like vp_prepare_geometry for frame sizes).
+
+  * full-depth Base at T = 48 and T = 64 (16 -> 48 / 64) and Large at T = 48 (8 -> 48) against
+    the fp64 oracle fixtures g9 / g10 / g11 (tests/golden/make_golden.py, same seeds): fp32
+    sampled tokens within the north_star 1e-5, bf16 L2-normalised token mean within 1e-3 and the
+    sampled-token mean-abs within 3e-2 (the bars of test_gpu_fullsize.py);
+  * full-depth LvT-Base at T = 40 against g12: the auxiliary encoder attends over all
+    T*N = 10240 tokens of the clip (encoders.py:846-857); fp32 within 2e-5, bf16 within the
+    reference's 1e-3 (frame embeddings 2e-3, as test_gpu_lvt_large.py);
+  * frame paddings at T = 40 and the classifier at T = 36 (reduced depth, oracle on the fly);
+  * the C-ABI contract: vp_forward at an unprepared T fails with VP_ESTATE before launching,
+    vp_prepare_frames validates T and is idempotent.
+
+Parity unpinned by the reference (JAX absent): the bar is the oracle.
+"""
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import videoprism_oracle as orc
+from videoprism import _native, encoders, models, params
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+LONG = {"base48": ("g9_base_t48.npz", "videoprism_public_v1_base", "videoprism_v1_base"),
+        "base64": ("g10_base_t64.npz", "videoprism_public_v1_base", "videoprism_v1_base"),
+        "large48": ("g11_large_t48.npz", "videoprism_public_v1_large", "videoprism_v1_large")}
+
+
+def _pool_l2(e):
+    m = e.astype(np.float64).mean(axis=1)
+    return m / np.sqrt((m * m).sum(-1, keepdims=True) + 1e-12)
+
+
+def _setup(which):
+    fname, model_name, cfg_key = LONG[which]
+    g = np.load(os.path.join(GOLD, fname), allow_pickle=False)
+    T = int(g["T"])
+    var = params.synthetic_params(models.CONFIGS[cfg_key], seed=int(g["param_seed"]))
+    video = np.random.default_rng(int(g["video_seed"])).random((1, T, 288, 288, 3), dtype=np.float32)
+    return g, T, var, video, model_name
+
+
+@pytest.mark.parametrize("which", ["base48", "base64", "large48"])
+def test_long_clip_full_depth_f32(cuda, which):
+    g, T, var, video, name = _setup(which)
+    emb, _ = models.get_model(name).apply(var, video, train=False)
+    assert emb.shape[:2] == (1, T * 256)
+    err = np.abs(emb[0, ::64] - g["rows_f64"])
+    perr = np.abs(_pool_l2(emb) - g["pooled_f64"]).max()
+    print(f"{which} f32 T={T}: sampled-token max-abs {err.max():.3e} mean-abs {err.mean():.3e}; pooled {perr:.3e}")
+    assert err.max() <= 1e-5
+
+
+@pytest.mark.parametrize("which", ["base48", "base64", "large48"])
+def test_long_clip_full_depth_bf16(cuda, which):
+    g, T, var, video, name = _setup(which)
+    emb, _ = models.get_model(name, fprop_dtype=torch.bfloat16).apply(var, video, train=False)
+    emb = np.asarray(emb, np.float64)
+    perr = np.abs(_pool_l2(emb) - g["pooled_f64"]).max()
+    rerr = np.abs(emb[0, ::64] - g["rows_f64"]).mean()
+    ferr = np.abs(emb[0].reshape(T, -1, emb.shape[-1]).mean(axis=1) - g["frame_mean_f64"]).max()
+    print(f"{which} bf16 T={T}: pooled max-abs {perr:.3e}; sampled-token mean-abs {rerr:.3e}; "
+          f"frame-mean max-abs {ferr:.3e}")
+    assert perr <= 1e-3 and rerr <= 3e-2
+
+
+@pytest.fixture(scope="module")
+def lvt_base_t40():
+    g = np.load(os.path.join(GOLD, "g12_lvt_base_t40.npz"), allow_pickle=False)
+    cfg = dict(models.CONFIGS[str(g["cfg"])])
+    cfg["vocabulary_size"] = int(g["vocabulary_size"])
+    var = params.synthetic_params(cfg, seed=int(g["param_seed"]), specs=params.clip_leaf_specs(cfg))
+    video = np.random.default_rng(int(g["video_seed"])).random((1, int(g["T"]), 288, 288, 3), dtype=np.float32)
+    return g, var, video
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_lvt_base_t40_full_depth(cuda, lvt_base_t40, bf16):
+    g, var, video = lvt_base_t40
+    mdl = models.get_model("videoprism_lvt_public_v1_base", fprop_dtype=torch.bfloat16 if bf16 else None)
+    mdl.vocabulary_size = int(g["vocabulary_size"])
+    v, t, out = mdl.apply(var, video, g["text_token_ids"], g["text_paddings"], train=False,
+                          return_intermediate=("frame_embeddings",))
+    v, t = np.asarray(v, np.float64), np.asarray(t, np.float64)
+    f = np.asarray(out["frame_embeddings"], np.float64)
+    ev = np.abs(v - g["video_emb_f64"]).max()
+    et = np.abs(t - g["text_emb_f64"]).max()
+    es = np.abs(v @ t.T - g["similarity_f64"]).max()
+    ef = np.abs(f - g["frame_emb_f64"]).max()
+    print(f"LvT-B T=40 {'bf16' if bf16 else 'f32'}: video {ev:.3e} text {et:.3e} similarity {es:.3e} "
+          f"frames {ef:.3e}")
+    assert f.shape == (1, 40, 768)
+    bar, fbar = (1e-3, 2e-3) if bf16 else (2e-5, 2e-5)
+    assert ev <= bar and et <= bar and es <= bar and ef <= fbar, (ev, et, es, ef)
+
+
+def _small_cfg():
+    cfg = dict(models.CONFIGS["videoprism_v1_base"])
+    cfg.update(num_spatial_layers=1, num_temporal_layers=1)
+    return cfg
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_long_clip_frame_paddings(cuda, bf16):
+    """T = 40 with the last 13 frames of clip 1 padded (encoders.py:440-447): the unfused
+    temporal attention with key paddings at S = 40."""
+    cfg = _small_cfg()
+    var = params.synthetic_params(cfg, seed=5)
+    T = 40
+    video = np.random.default_rng(6).random((2, T, 144, 144, 3), dtype=np.float32)
+    fp = np.zeros((2, T), np.float32)
+    fp[1, 27:] = 1.0
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedEncoder(**cfg),
+                         fprop_dtype=torch.bfloat16 if bf16 else None)
+    emb, _ = m.apply(var, video, frame_paddings=fp)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, "f64", frame_paddings=fp)
+    emb = np.asarray(emb, np.float64)
+    if bf16:
+        perr = np.abs(orc.l2_normalize(emb.mean(1)) - orc.l2_normalize(ref.mean(1))).max()
+        mean_err = np.abs(emb - ref).mean()
+        print(f"paddings bf16 T={T}: pooled {perr:.3e} token mean-abs {mean_err:.3e}")
+        assert perr <= 1e-3 and mean_err <= 2e-2
+    else:
+        err = np.abs(emb - ref).max()
+        print(f"paddings f32 T={T}: max-abs {err:.3e}")
+        assert err <= 1e-5
+
+
+def test_long_clip_classifier(cuda):
+    """FactorizedVideoClassifier (encoders.py:583-653) at T = 36, Base dims 1+1 layers, fp32."""
+    enc = _small_cfg()
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedVideoClassifier(encoder_params=enc,
+                                                                                  num_classes=10))
+    var = params.synthetic_params(enc, 7, specs=m.param_specs())
+    video = np.random.default_rng(8).random((1, 36, 144, 144, 3), dtype=np.float32)
+    logits, _ = m.apply(var, video)
+    ref, _ = orc.video_classifier(var["params"], enc, video, "f64")
+    err = np.abs(np.asarray(logits, np.float64) - ref).max()
+    print(f"classifier f32 T=36: logits max-abs {err:.3e}")
+    assert err <= 1e-5 * max(1.0, np.abs(ref).max())
+
+
+def _raw_handle(cfg, var):
+    lib = _native.load()
+    c = _native.vp_config(patch_size=cfg["patch_size"], pos_emb_t=cfg["pos_emb_shape"][0],
+                          pos_emb_h=cfg["pos_emb_shape"][1], pos_emb_w=cfg["pos_emb_shape"][2],
+                          model_dim=cfg["model_dim"], num_spatial_layers=cfg["num_spatial_layers"],
+                          num_temporal_layers=cfg["num_temporal_layers"], num_heads=cfg["num_heads"],
+                          mlp_dim=cfg["mlp_dim"], atten_logit_cap=float(cfg["atten_logit_cap"]),
+                          fprop_dtype=_native.VP_F32)
+    h = ctypes.c_void_p()
+    _native.check(lib.vp_create(ctypes.byref(c), torch.cuda.current_device(), ctypes.byref(h)))
+    for name, arr in params.flatten(var["params"]).items():
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+        _native.check(lib.vp_set_param(h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), shape, a.ndim))
+    _native.check(lib.vp_finalize(h))
+    return lib, h
+
+
+def test_prepare_frames_contract(cuda):
+    cfg = _small_cfg()
+    var = params.synthetic_params(cfg, seed=9)
+    lib, h = _raw_handle(cfg, var)
+    try:
+        B, T, H = 1, 33, 144
+        n = ctypes.c_size_t()
+        _native.check(lib.vp_workspace_bytes(h, B, T, H, H, ctypes.byref(n)))
+        ws = torch.empty(n.value, dtype=torch.uint8, device=cuda)
+        _native.check(lib.vp_prepare_geometry(h, H, H))
+        video = torch.rand((B, T, H, H, 3), device=cuda)
+        out = torch.full((B, T * 64, 768), 7.0, device=cuda)
+        args = (h, ctypes.c_void_p(video.data_ptr()), _native.VP_F32, B, T, H, H, None,
+                ctypes.c_void_p(out.data_ptr()), _native.VP_F32, None, ctypes.c_void_p(ws.data_ptr()),
+                ws.numel(), None)
+        rc = lib.vp_forward(*args)
+        torch.cuda.synchronize()
+        assert rc == _native.VP_ESTATE and b"vp_prepare_frames" in lib.vp_last_error()
+        assert bool((out == 7.0).all())  # refused before the first launch
+        assert lib.vp_prepare_frames(h, 0) == _native.VP_EINVAL
+        for T_ in (33, 33, 16, 1):  # idempotent; precomputed lengths are a no-op
+            assert lib.vp_prepare_frames(h, T_) == _native.VP_OK
+        assert lib.vp_forward(*args) == _native.VP_OK
+        torch.cuda.synchronize()
+        ref, _ = orc.factorized_encoder(var["params"], video.cpu().numpy(), cfg, "f64")
+        err = np.abs(out.cpu().numpy().astype(np.float64) - ref.reshape(out.shape)).max()
+        assert err <= 1e-5, err
+    finally:
+        lib.vp_destroy(h)

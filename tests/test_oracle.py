@@ -199,3 +199,22 @@ def test_oracle_f32_and_bf16_modes_close_to_f64():
     ebf, _ = orc.factorized_encoder(var["params"], x, TINY, "bf16")
     assert np.abs(e32 - e64).max() < 1e-5
     assert 1e-4 < np.abs(ebf - e64).max() < 0.2
+
+
+@pytest.mark.parametrize("mode", ["f64", "bf16"])
+def test_dot_atten_query_blocks_equal_whole(monkeypatch, mode):
+    """Long sequences run the oracle's attention in query blocks (the LvT auxiliary encoder over
+    T*N = 10240 tokens would need 10 GB of fp64 logits at once); each query row's softmax is
+    independent of the others, so the blocked form equals the whole one, with key paddings too."""
+    rng = np.random.default_rng(11)
+    B, S, N, H = 2, 37, 3, 8
+    q, k, v = (rng.normal(0, 1.0, (B, S, N, H)) for _ in range(3))
+    pad = np.zeros((B, S))
+    pad[1, 30:] = 1.0
+    nm = orc.Numerics(mode)
+    for mask in (None, orc.padding_mask(pad), orc.attention_masks_for_fprop(pad, True)):
+        whole = orc.dot_atten(q, k, v, mask, nm, 50.0, H)
+        monkeypatch.setattr(orc, "_ATTN_CHUNK_ELEMS", B * N * S * 5)  # 5 query rows per block
+        blocked = orc.dot_atten(q, k, v, mask, nm, 50.0, H)
+        monkeypatch.undo()
+        np.testing.assert_allclose(blocked, whole, rtol=0, atol=1e-14 if mode == "f64" else 0)

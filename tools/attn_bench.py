@@ -1,13 +1,13 @@
 """Spatial attention microbenchmark at the bench shape (B=32 clips x 16 frames = 512 sequences
 of 256 tokens, 12 heads): the production kernel against a q|k|v-sized copy (the memory stream's
-ceiling) and, with QH=1, the half-frame experiment kernel of the diag library; interleaved rounds in
-one process.  (The ablation builds that priced its parts are recorded in DESIGN.md §4; their
-sources are in git history.)"""
+ceiling); interleaved rounds in one process.  `long`: the LvT auxiliary attention and its diag-library
+A/B builds.  (The ablation builds and the half-frame kernel that priced its parts are recorded in
+profiles/HISTORY.md; their sources are in git history.)"""
 import os
 import sys
 
-if os.environ.get("QH") or sys.argv[1:2] == ["long"]:
-    os.environ.setdefault("VP_DIAG_LIB", "1")  # the half-frame kernel lives in the diag library
+if sys.argv[1:2] == ["long"]:
+    os.environ.setdefault("VP_DIAG_LIB", "1")  # the A/B builds live in the diag library
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
@@ -38,16 +38,7 @@ def main():
     qkv[:, :D] *= 0.125
     qkv = qkv.to(torch.bfloat16)
     o = torch.empty((nseq * S, D), device=dev, dtype=torch.bfloat16)
-    st = lambda: torch.cuda.current_stream().cuda_stream
     fns = {"prod": lambda: nat.op_attention(qkv, nseq, S, heads, 50.0, out=o)}
-    if os.environ.get("QH"):  # half-frame workgroups, K/V in two 128-key chunks (attention_qh.hip)
-        o2 = torch.empty_like(o)
-        nat.op_attention(qkv, nseq, S, heads, 50.0, out=o)
-        nat.call("vp_dev_attention_qh", qkv.data_ptr(), o2.data_ptr(), nseq, heads, 50.0, st())
-        torch.cuda.synchronize()
-        print("qh == prod (bitwise):", bool(torch.equal(o, o2)),
-              "max diff", float((o.float() - o2.float()).abs().max()), flush=True)
-        fns["qh"] = lambda: nat.call("vp_dev_attention_qh", qkv.data_ptr(), o2.data_ptr(), nseq, heads, 50.0, st())
     # streaming reference: read the q|k|v buffer and write a same-size copy (2 x 604 MB)
     cp = torch.empty_like(qkv)
     fns["copy"] = lambda: cp.copy_(qkv)

@@ -2,15 +2,15 @@
 8-wave `gemm_bf16`) with the forward's epilogues, against torch.matmul (hipBLASLt) as a
 known-good reference on the same device and data (no epilogue on the torch side).
 
-  python tools/gemm_bench.py            # kernels vs torch, plus w4 == w8 / ov == w4 bitwise checks
+  python tools/gemm_bench.py            # kernels vs torch, plus the w4 == w8 bitwise check
   python tools/gemm_bench.py ablate     # the 4-wave kernel's ablation builds (diag library: no
                                         # ds_reads / no staging loads / no epilogue), 2-stage and S3
   python tools/gemm_bench.py fold       # LN-folded / row-statistics epilogues vs the plain ones
   python tools/gemm_bench.py msize      # the FFN GEMMs at smaller M (Infinity-Cache resident A)
-  python tools/gemm_bench.py w8b        # 8-wave kernel with the 4-wave pipeline vs the 4-wave one
   python tools/gemm_bench.py tattn      # fused temporal attention launches vs their no-epilogue builds
-(Round-1..3 experiments -- early loads, prefetch distances, start skew, tile orders, XCD pairs,
-plain stores -- are recorded in DESIGN.md §4 with their numbers; their builds are in git history.)
+(Rounds 1-4 experiments -- early loads, prefetch distances, start skew, tile orders, XCD pairs, plain
+stores, the overlapped-epilogue and 8-wave/4-wave-pipeline kernels -- are recorded in
+profiles/HISTORY.md with their numbers; their builds are in git history.)
 """
 import ctypes
 import os
@@ -68,22 +68,15 @@ def compare(dev, g):
         same = bool(torch.equal(outs[4], outs[8]))
         del outs
         o = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        o2 = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        nat.dev_gemm_ov(a, w, b, epi, o2, resid=o2 if resid else None)
-        o4 = x0.clone() if resid else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        nat.dev_gemm_kernel(4, a, w, b, epi, o4, resid=o4 if resid else None)
-        same_ov = bool(torch.equal(o2, o4))
-        del o2, o4
         fns = {"w8": lambda: nat.dev_gemm_kernel(8, a, w, b, epi, o, resid=o if resid else None),
                "w4": lambda: nat.dev_gemm_kernel(4, a, w, b, epi, o, resid=o if resid else None),
-               "ov": lambda: nat.dev_gemm_ov(a, w, b, epi, o, resid=o if resid else None),
                "torch": lambda: torch.matmul(a, w.t())}
         res = {k: [] for k in fns}
         for _ in range(3):  # interleaved rounds
             for k, f in fns.items():
                 res[k].append(timeit(f))
         flop = 2.0 * M * N * K
-        print(f"{name:5s} M={M} N={N} K={K} epi={epi} w4==w8:{same} ov==w4:{same_ov}: " + " | ".join(
+        print(f"{name:5s} M={M} N={N} K={K} epi={epi} w4==w8:{same}: " + " | ".join(
             f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
 
 
@@ -147,35 +140,6 @@ def msize(dev, g):
             del a, o, part, rs
 
 
-def w8b_ab(dev, g):
-    """8-wave kernel with the 4-wave pipeline (gemm_bf16_w8b.hip) vs the 4-wave kernel: ffn_layer1's
-    production epilogue (LN fold + GELU), the plain epilogue and no epilogue, at the forward's shapes."""
-    for name, M, N, K in (("ffn1", M_TOK, 3072, 768), ("qkv", M_TOK, 2304, 768), ("ffn1-large", 65536, 4096, 1024)):
-        a, w, b = operands(M, N, K, g, dev)
-        o1 = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
-        o2 = torch.empty_like(o1)
-        rs = torch.stack([torch.ones(M, device=dev), torch.zeros(M, device=dev)], 1).contiguous()
-        c = torch.zeros(N, device=dev)
-        nat.dev_gemm_ln(a, w, b, nat.EPI_GELU_LN, o1, ln_rs=rs, ln_c=c)
-        nat.dev_gemm_w8b(a, w, b, nat.EPI_GELU_LN, o2, ln_rs=rs, ln_c=c)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(o1, o2))
-        fns = {"w4-gelu-ln": lambda: nat.dev_gemm_ln(a, w, b, nat.EPI_GELU_LN, o1, ln_rs=rs, ln_c=c),
-               "w8b-gelu-ln": lambda: nat.dev_gemm_w8b(a, w, b, nat.EPI_GELU_LN, o2, ln_rs=rs, ln_c=c),
-               "w4-bf16": lambda: nat.dev_gemm_kernel(4, a, w, b, 0, o1),
-               "w8b-bf16": lambda: nat.dev_gemm_w8b(a, w, b, 0, o2),
-               "w4-noepi": lambda: nat.dev_gemm_w4_abl(a, w, b, o1, 8),
-               "w8b-noepi": lambda: nat.dev_gemm_w8b(a, w, b, 0, o2, diag=8)}
-        res = {k: [] for k in fns}
-        for _ in range(3):
-            for k, f in fns.items():
-                res[k].append(timeit(f, iters=10, warm=2))
-        flop = 2.0 * M * N * K
-        print(f"{name} w8b==w4 (gelu-ln): {same}: " + " | ".join(
-            f"{k} {min(v)*1e3:7.1f} us {flop/min(v)/1e9:7.1f} TF" for k, v in res.items()), flush=True)
-        del a, w, o1, o2
-
-
 def tattn(dev, g):
     """The fused temporal attention launches at the bench shape (M = 131072, D = 768, 12 heads): product
     builds and their no-epilogue builds (diag ABL 8, prices the epilogues); interleaved rounds."""
@@ -208,7 +172,7 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     mode = sys.argv[1] if len(sys.argv) > 1 else ""
-    modes = {"fold": folded, "ablate": ablate, "msize": msize, "w8b": w8b_ab, "tattn": tattn}
+    modes = {"fold": folded, "ablate": ablate, "msize": msize, "tattn": tattn}
     modes.get(mode, compare)(dev, g)
 
 

@@ -91,7 +91,7 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
 
 hipError_t gemm_bf16_w4_video(int epi, const bf16_t* video, int P, const bf16_t* W, int M, int N, const EpiArgs& ep,
                               hipStream_t s) {
-  if (P < 3 || 3 * P > 64 || M % BM || N % BN) return hipErrorInvalidValue;
+  if (!video_patch_ok(P) || M % BM || N % BN) return hipErrorInvalidValue;
   const int64_t lda = 16LL * P * 3;  // elements of one pixel row
   const int K = video_patch_k(P);
   if ((uint64_t)(M / BM) * 16 * P * lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * K * 2 >= 0xFFFFFFF0ull)

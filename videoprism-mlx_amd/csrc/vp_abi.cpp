@@ -20,6 +20,31 @@
 
 using namespace vpi;
 
+namespace {
+
+// the temporal positional table for T frames, [T][D]: temporal_pos_emb/emb_var itself when T ==
+// pos_emb_t, else _interpolate_emb_1d (encoders.py:107-130: jax.image.resize 'bilinear', antialiased
+// when shrinking), fp64 on the host
+std::vector<float> temporal_table(const vp_handle* h, int T) {
+  const int64_t D = h->cfg.model_dim;
+  const int Tp = h->cfg.pos_emb_t;
+  const std::vector<float>& e = h->temporal_pos_host;
+  std::vector<float> dst((size_t)T * D);
+  if (T == Tp) {
+    std::memcpy(dst.data(), e.data(), (size_t)T * D * 4);
+    return dst;
+  }
+  const auto w = resize_weights(Tp, T);
+  for (int t = 0; t < T; ++t)
+    for (int64_t d = 0; d < D; ++d) {
+      double s = 0.0;
+      for (int i = 0; i < Tp; ++i) s += w[(size_t)i * T + t] * e[(size_t)i * D + d];
+      dst[(size_t)t * D + d] = (float)s;
+    }
+  return dst;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -116,7 +141,7 @@ int vp_finalize(vp_handle* h) {
     for (int64_t i = 0; i < kreal; ++i)
       for (int64_t n = 0; n < D; ++n) t[(size_t)n * h->kpad + i] = k[(size_t)i * D + n];
     if ((rc = upload_mat(h, t, &h->wpatch))) return rc;
-    if (is_bf16(h) && P >= 3 && 3 * P <= 64) {  // the frames' chunk order (gemm_bf16_w4_video, vp_kernels.h)
+    if (is_bf16(h) && vp::video_patch_ok((int)P)) {  // the frames' chunk order (gemm_bf16_w4_video, vp_kernels.h)
       const int64_t cpr = vp::video_patch_cpr((int)P), kv = vp::video_patch_k((int)P);
       std::vector<float> tv((size_t)D * kv, 0.0f);
       for (int64_t py = 0; py < P; ++py)
@@ -134,25 +159,18 @@ int vp_finalize(vp_handle* h) {
   }
   if ((rc = upload_f32(h, param_data(h, px + "spatial_pos_emb/emb_var"), &h->spatial_pos))) return rc;
   h->spatial_pos_host = param_data(h, px + "spatial_pos_emb/emb_var");
-  {  // temporal positional tables for every T in 1..kMaxT (encoders.py:543-553)
-    const auto& e = param_data(h, px + "temporal_pos_emb/emb_var");
-    const int Tp = c.pos_emb_t;
-    std::vector<float> tab((size_t)(kMaxT + 1) * kMaxT * D, 0.0f);
-    for (int T = 1; T <= kMaxT; ++T) {
-      float* dst = tab.data() + (size_t)T * kMaxT * D;
-      if (T == Tp) {
-        std::memcpy(dst, e.data(), (size_t)T * D * 4);
-      } else {
-        const auto w = resize_weights(Tp, T);
-        for (int t = 0; t < T; ++t)
-          for (int64_t d = 0; d < D; ++d) {
-            double s = 0.0;
-            for (int i = 0; i < Tp; ++i) s += w[(size_t)i * T + t] * e[(size_t)i * D + d];
-            dst[(size_t)t * D + d] = (float)s;
-          }
-      }
+  {  // temporal positional tables for T = 1..kPrecomputedT in one buffer (encoders.py:543-553)
+    h->temporal_pos_host = param_data(h, px + "temporal_pos_emb/emb_var");
+    std::vector<float> tab;
+    std::vector<size_t> off(kPrecomputedT + 1);
+    for (int T = 1; T <= kPrecomputedT; ++T) {
+      off[T] = tab.size();
+      const std::vector<float> t = temporal_table(h, T);
+      tab.insert(tab.end(), t.begin(), t.end());
     }
-    if ((rc = upload_f32(h, tab, &h->temporal_pos))) return rc;
+    float* dev = nullptr;
+    if ((rc = upload_f32(h, tab, &dev))) return rc;
+    for (int T = 1; T <= kPrecomputedT; ++T) h->temporal_pos[T] = dev + off[T];
   }
   const bool fold = is_bf16(h);
   if ((rc = pack_stack(h, px + "spatial_encoder/transformers_stack/x_layers/", c.num_spatial_layers, D, c.mlp_dim,
@@ -216,6 +234,19 @@ int vp_prepare_geometry(vp_handle* h, int64_t H, int64_t W) {
   return VP_OK;
 }
 
+int vp_prepare_frames(vp_handle* h, int64_t T) {
+  if (!h) return fail(VP_EINVAL, "null handle");
+  if (!h->finalized) return fail(VP_ESTATE, "vp_finalize has not been called");
+  if (T < 1 || T > (int64_t)1 << 20) return fail(VP_EINVAL, "T must be in [1, 2^20]");
+  if (h->temporal_pos.count((int)T)) return VP_OK;
+  VP_HIP(hipSetDevice(h->device));
+  float* dev = nullptr;
+  int rc = upload_f32(h, temporal_table(h, (int)T), &dev);
+  if (rc) return rc;
+  h->temporal_pos[(int)T] = dev;
+  return VP_OK;
+}
+
 int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W,
                        size_t* bytes) {
   if (!h || !bytes) return fail(VP_EINVAL, "null argument");
@@ -253,6 +284,10 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
       return fail(VP_ESTATE, "patch grid differs from pos_emb_shape[1:]: call vp_prepare_geometry first");
     sp_pos = it->second;
   }
+  const auto tp = h->temporal_pos.find((int)T);
+  if (tp == h->temporal_pos.end())
+    return fail(VP_ESTATE, "no temporal positional table for T = " + std::to_string(T) + ": call vp_prepare_frames first");
+  const float* tpos = tp->second;
   const int D = c.model_dim, F = c.mlp_dim, NH = c.num_heads;
   const size_t es = bf ? 2 : 4;
   char* ws = static_cast<char*>(workspace);
@@ -296,7 +331,10 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
   // bf16 on a 16x16 patch grid: the patch embedding reads the frames themselves (no patch
   // tensor); f32 / uint8 frames are converted to bf16 frames first (the patchify kernels' per-value
   // conversion, so every input dtype gives bitwise the bf16 caller's result)
-  if (h->wpatch_v && H / P_ == 16 && W / P_ == 16 && Mp == M) {
+  // the fused path reads bf16 frames in 16-B chunks at 4-B granularity, and video_to_bf16 reads
+  // float4 / uchar4: frames at a less aligned address (a sliced caller buffer) take patchify + GEMM
+  const uintptr_t vmis = reinterpret_cast<uintptr_t>(video) & (in_dtype == VP_F32 ? 15 : 3);
+  if (h->wpatch_v && H / P_ == 16 && W / P_ == 16 && Mp == M && vmis == 0) {
     const bf16_t* frames = static_cast<const bf16_t*>(video);
     if (in_dtype != VP_BF16) {
       VP_HIP(f.rec(PC_PATCHIFY, 0.0, dM * kreal * (in_es + dE), [&] {
@@ -331,7 +369,6 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
   if (spatial_out)
     VP_HIP(rec(PC_LAYERNORM, 0.0, dM * dD * dE + dM * dD * (out_dtype == VP_BF16 ? 2 : 4), [&] {
       return layernorm(x, bf, M, D, h->sln_g, h->sln_b, spatial_out, out_dtype == VP_BF16, PERM_NONE, 1, 1, nullptr, s); }));
-  const float* tpos = h->temporal_pos + (size_t)T * kMaxT * D;
   VP_HIP(rec(PC_LAYERNORM, 0.0, ln_bytes, [&] {
     return layernorm(x, bf, M, D, h->sln_g, h->sln_b, x2, bf, PERM_BTN_TO_BNT, (int)T, Nsp, tpos, s,
                      bf && c.num_temporal_layers > 0 ? ln_rs : nullptr); }));
@@ -561,8 +598,8 @@ int vp_dev_gemm_tattn(int which, const void* A, const void* W, int64_t M, int64_
 int vp_dev_patch_embed(const void* video, int64_t frames, int64_t P, const void* wv, int64_t N, const float* bias,
                        const float* pos, void* out, void* stream) {
   using namespace vp;
-  if (!video || !wv || !bias || !pos || !out || frames < 1 || P < 3 || 3 * P > 64 || N % 256)
-    return fail(VP_EINVAL, "bad argument");
+  if (!video || !wv || !bias || !pos || !out || frames < 1 || N % 256) return fail(VP_EINVAL, "bad argument");
+  if (!video_patch_ok((int)P)) return fail(VP_EINVAL, "fused patch embedding needs an even patch size, 4 <= P <= 21");
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.pos = pos; ep.pos_rows = 256;
   VP_HIP(gemm_bf16_w4_video(EPI_POS_BF16, (const bf16_t*)video, (int)P, (const bf16_t*)wv, (int)(frames * 256), (int)N,

@@ -107,7 +107,9 @@ struct LayerW {  // one transformer layer, packed
   float* cqkv_blk = nullptr;
 };
 
-constexpr int kMaxT = 32;
+// temporal positional tables precomputed by vp_finalize (T = 1..kPrecomputedT); longer clips get
+// theirs from vp_prepare_frames (encoders.py:543-553 interpolates to any T)
+constexpr int kPrecomputedT = 32;
 
 enum ProfClass {
   PC_PATCHIFY = 0, PC_GEMM_PATCH, PC_LAYERNORM, PC_GEMM_QKV, PC_ATTN_SPATIAL, PC_ATTN_TEMPORAL,
@@ -145,13 +147,14 @@ struct vp_handle {
   // packed device weights
   int kpad = 0;
   void* wpatch = nullptr;      // [D][kpad]
-  void* wpatch_v = nullptr;    // bf16, 3 <= P <= 21: [D][video_patch_k(P)] in the frames' chunk order (fused
+  void* wpatch_v = nullptr;    // bf16, vp::video_patch_ok(P) (even P, 4..20): [D][video_patch_k(P)] in the frames' chunk order (fused
                                // patch embedding straight from the frames, gemm_bf16_w4_video)
   float* bpatch = nullptr;
   float* spatial_pos = nullptr;    // [pos_h*pos_w][D]
   std::vector<float> spatial_pos_host;                   // kept for other patch grids
   std::map<std::pair<int, int>, float*> grid_pos;        // interpolated tables (vp_prepare_geometry)
-  float* temporal_pos = nullptr;   // [kMaxT+1][kMaxT][D]: table for T at offset T*kMaxT*D
+  std::vector<float> temporal_pos_host;                  // temporal_pos_emb/emb_var [pos_t][D]
+  std::map<int, float*> temporal_pos;                    // T -> [T][D] (resampled when T != pos_t)
   std::vector<vpi::LayerW> spatial, temporal;
   float *sln_g = nullptr, *sln_b = nullptr, *tln_g = nullptr, *tln_b = nullptr;
   vpi::Profiler prof;
@@ -451,7 +454,6 @@ inline int check_geometry(const vp_handle* h, int64_t B, int64_t T, int64_t H, i
   if (H % P || W % P)
     return fail(VP_EINVAL, "Image height (" + std::to_string(H) + ") and width (" + std::to_string(W) +
                                ") should be multiples of patch_size (" + std::to_string(P) + ").");
-  if (T > kMaxT) return fail(VP_ENOTSUP, "T > 32 frames not supported");
   if (chunk_clips(h->cfg, T, H, W) < 1)
     return fail(VP_ENOTSUP, "one clip of " + std::to_string(T) + "x" + std::to_string(H) + "x" + std::to_string(W) +
                                 " exceeds the GEMM operand range (4 GiB per operand)");
@@ -470,8 +472,9 @@ namespace vpi {
 // The bf16 attention kernels compute the capped softmax without a running max: every numerator
 // is exp(l) with |l| <= cap, and both the row sum and the unnormalised O = sum_s exp(l_s) v_s are
 // accumulated in fp32.  With cap <= 50 (the reference's value for every VideoPrism config,
-// models.py:91) and S <= 4096 keys, |O| <= e^50 * 4096 * max|v| stays below FLT_MAX for any
-// |v| < 1.6e13 -- bf16 activations of a trained model are nowhere near.  (Round 2 allowed 80,
+// models.py:91) and S keys, |O| <= e^50 * S * max|v| stays below FLT_MAX for any |v| < 1.6e13 at
+// S = 4096 (16 frames) and |v| < 1e12 at S = 65536 (256 frames of the auxiliary encoder) --
+// bf16 activations of a trained model are nowhere near.  (Round 2 allowed 80,
 // priced on the row sum alone: e^80 * S * |v| overflows for |v| > ~1.5 at S = 4096.)  Any other
 // cap (<= 0: no capping, layers.py:586-589; > 50) takes the online-softmax kernel.
 constexpr float kMaxFastCap = 50.0f;

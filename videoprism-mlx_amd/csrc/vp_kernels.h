@@ -102,6 +102,11 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
 // predecessor and in the slots j >= cpr (zeros; video_patch_w packs it)
 inline int video_patch_cpr(int P) { return (3 * P + 7) / 8; }
 inline int video_patch_k(int P) { return 64 * P; }
+// patch sizes the fused path takes: a patch pixel row (3P values) fits one 64-wide K-tile, and P is
+// even so every 16-B chunk starts 4-B aligned in the frame (byte offsets 6P px + 16 j and 6P - 16 for
+// the overlapping last chunk; P = 18 is the models' size).  Odd P would put chunks at 2-B offsets:
+// those grids take patchify + GEMM instead
+inline bool video_patch_ok(int P) { return P >= 4 && P % 2 == 0 && 3 * P <= 64; }
 hipError_t gemm_bf16_w4_video(int epi, const bf16_t* video, int P, const bf16_t* W, int M, int N, const EpiArgs& ep,
                               hipStream_t s);
 // N-tile group size of the persistent tile order (gemm_bf16_w4.hip; shared by the diag kernels)

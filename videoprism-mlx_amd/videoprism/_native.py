@@ -73,6 +73,7 @@ _SIGNATURES = {
     "vp_param_name": (c_int, [c_void_p, c_int, POINTER(c_char_p)]),
     "vp_finalize": (c_int, [c_void_p]),
     "vp_prepare_geometry": (c_int, [c_void_p, c_int64, c_int64]),
+    "vp_prepare_frames": (c_int, [c_void_p, c_int64]),
     "vp_workspace_bytes": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "vp_forward": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p,
                            c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -147,18 +148,11 @@ _SIGNATURES = {
 }
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
-    "vp_dev_gemm_w8b": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
-                                c_void_p, c_void_p, c_void_p, c_void_p]),
-    "vp_dev_attention_qh": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_attention_long_var": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_tattn_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_w4_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                    c_void_p, c_void_p]),
-    "vp_dev_gemm_ov": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
-                               c_void_p, c_void_p]),
-    "vp_dev_qkv_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                     c_int64, c_int64, c_float, c_void_p]),
 }
 
 _lib = None
@@ -301,16 +295,6 @@ def dev_gemm_ln(a, w, bias, epilogue, out, resid=None, pos=None, rowpad=None, ln
     return out
 
 
-def dev_gemm_w8b(a, w, bias, epilogue, out, rowpad=None, ln_rs=None, ln_c=None, diag=0, stream=None):
-    """Diag library only: the 8-wave bf16 GEMM (tools/diag/csrc/gemm_bf16_w8b.hip), EPI_STORE or
-    EPI_GELU_LN; all tensors contiguous on the device; diag 8 = no epilogue (timing only)."""
-    M, K = a.shape
-    N = w.shape[0]
-    call("vp_dev_gemm_w8b", epilogue, diag, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(rowpad),
-         _ptr(ln_rs), _ptr(ln_c), _stream(stream))
-    return out
-
-
 def dev_gemm_w4_abl(a, w, bias, out, abl, s3=False, stream=None):
     """Diag library only: an ablation build of the product 4-wave GEMM (EPI_BF16; abl 2 = no
     ds_reads, 4 = no staging loads, 8 = no epilogue) -- timing only, results garbage."""
@@ -318,23 +302,6 @@ def dev_gemm_w4_abl(a, w, bias, out, abl, s3=False, stream=None):
     N = w.shape[0]
     call("vp_dev_gemm_w4_abl", abl, 1 if s3 else 0, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias),
          _stream(stream))
-    return out
-
-
-def dev_gemm_ov(a, w, bias, epilogue, out, resid=None, stream=None):
-    """Diag library only: the overlapped-epilogue GEMM (tools/diag/csrc/gemm_bf16_ov.hip)."""
-    M, K = a.shape
-    N = w.shape[0]
-    call("vp_dev_gemm_ov", epilogue, _ptr(a), _ptr(w), M, N, K, _ptr(out), _ptr(bias), _ptr(resid),
-         _stream(stream))
-    return out
-
-
-def dev_qkv_attention(x, ln_rs, wqkv, bias, lnc, out, frames, heads, cap, stream=None):
-    """Fused q|k|v projection (LN1 folded) + spatial attention: x [frames*256, D] bf16 ->
-    out [frames*256, D] bf16; all tensors contiguous on the device."""
-    call("vp_dev_qkv_attention", _ptr(x), _ptr(ln_rs), _ptr(wqkv), _ptr(bias), _ptr(lnc), _ptr(out),
-         frames, heads, float(cap), _stream(stream))
     return out
 
 

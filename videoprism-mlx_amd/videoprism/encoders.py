@@ -79,6 +79,18 @@ def _profile_read(handle) -> dict:
     return out
 
 
+def _prepare_shape(handle, seen: set, H: int, W: int, T: int) -> None:
+    """First sight of a frame size / clip length: the interpolated spatial (encoders.py:497-512)
+    and temporal (:543-553) positional tables, cached on the device by the library (the
+    forward itself never allocates)."""
+    if (H, W) not in seen:
+        _native.call("vp_prepare_geometry", handle, H, W)
+        seen.add((H, W))
+    if T not in seen:
+        _native.call("vp_prepare_frames", handle, T)
+        seen.add(T)
+
+
 class Engine:
     """One vp_handle (packed weights on one device) plus a reusable workspace."""
 
@@ -162,9 +174,7 @@ class Engine:
                              f"of patch_size ({P}).")
         N = (H // P) * (W // P)
         D = self.cfg["model_dim"]
-        if (H, W) not in self._grids:  # interpolated spatial pos-emb for this frame size
-            _native.call("vp_prepare_geometry", self._h, H, W)
-            self._grids.add((H, W))
+        _prepare_shape(self._h, self._grids, H, W, T)
         if out is None:
             out = torch.empty((B, T * N, D), dtype=out_dtype, device=video.device)
         else:  # the kernels write B*T*N*D elements through the raw pointer
@@ -378,9 +388,7 @@ class ClipEngine:
         in_dt = _native._prec(video)  # uint8 frames are normalised /255 on device
         D = self.cfg["model_dim"]
         N = (H // P) * (W // P)
-        if (H, W) not in self._grids:
-            _native.call("vp_prepare_geometry", self.video_handle(), H, W)
-            self._grids.add((H, W))
+        _prepare_shape(self.video_handle(), self._grids, H, W, T)
         fdt = torch.bfloat16 if self.bf16 else torch.float32
         dev = video.device
         vemb = torch.empty((B, D), dtype=torch.float32, device=dev)
@@ -608,9 +616,7 @@ class ClassifierEngine:
         if video.dtype not in (torch.bfloat16, torch.float32, torch.uint8):
             video = video.float()
         in_dt = _native._prec(video)
-        if (H, W) not in self._grids:
-            _native.call("vp_prepare_geometry", self.video_handle(), H, W)
-            self._grids.add((H, W))
+        _prepare_shape(self.video_handle(), self._grids, H, W, T)
         D, N = self.cfg["model_dim"], (H // P) * (W // P)
         dev = video.device
         fdt = torch.bfloat16 if self.bf16 else torch.float32
