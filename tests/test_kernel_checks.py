@@ -126,3 +126,25 @@ def test_every_source_kernel_has_device_code(tmp_path):
     extra.write_text("__global__ __launch_bounds__(64) void not_built_kernel(float* o) { o[0] = 1.f; }\n")
     assert ck.missing_kernels(lib, srcs + [str(extra)]) == ["not_built_kernel"]
 
+
+
+@pytest.mark.parametrize("listing", ["attention.s"])
+def test_audit_rejects_a_wait_count_too_high(audited_asm, tmp_path, listing):
+    """vmcnt retires in issue order: the wait statement that retires the form-(ii) Q loads must leave
+    at most the younger LDS-DMA pieces outstanding.  With its count raised by 4 the oldest Q loads are
+    still in flight when the MFMAs read them, and the audit (which queues every vector-memory
+    instruction in issue order) refuses the listing.  (attention_long.s is not a negative case: its
+    chunk loop opens with a wait of its own that retires the Q loads before any MFMA reads them.)"""
+    src = [a for a in audited_asm if a.endswith(listing)][0]
+    assert ck.audit_asm(src) == []
+    lines = open(src).read().splitlines()
+    first_load = next(i for i, l in enumerate(lines)
+                      if l.strip().startswith("global_load_dwordx4") and lines[i - 1].strip() == ";;#ASMSTART")
+    k = next(i for i in range(first_load, len(lines)) if re.match(r"\s*s_waitcnt vmcnt\(\d+\)\s*$", lines[i])
+             and lines[i - 1].strip() == ";;#ASMSTART")
+    n = int(re.search(r"vmcnt\((\d+)\)", lines[k]).group(1))
+    lines[k] = lines[k].replace(f"vmcnt({n})", f"vmcnt({n + 4})")
+    bad = tmp_path / listing
+    bad.write_text("\n".join(lines) + "\n")
+    v = ck.audit_asm(str(bad))
+    assert v and "in flight" in v[0], v

@@ -33,7 +33,11 @@ _MSGPACK = None
 def _msgpack():
     global _MSGPACK
     if _MSGPACK is None:
-        import msgpack
+        try:
+            import msgpack
+        except ImportError as e:  # the AMDGPU metadata note is a msgpack map
+            raise SystemExit("check_kernels: the Python module 'msgpack' is required to read the kernels' "
+                             "AMDGPU metadata (pip install msgpack); the library was not checked") from e
         _MSGPACK = msgpack
     return _MSGPACK
 
@@ -209,17 +213,44 @@ def _kind(mn: str):
     return "lgkm" if mn.startswith("ds_") else "vm"
 
 
+_VMEM_MN = re.compile(r"^(global|buffer|flat|scratch)_(load|store|atomic)\w*")
+_WAIT_CNT = re.compile(r"(vmcnt|lgkmcnt)\((\d+)\)")
+
+
 def audit_asm(path: str):
     """Walk a hipcc -S listing in layout order and report any access to the destination registers
-    of a form-(ii) asm load between the load and the wait that retires it."""
+    of a form-(ii) asm load between the load and the wait that retires it.
+
+    vmcnt retires in issue order: every vector-memory instruction (loads, stores, LDS-DMA pieces;
+    the compiler's and asm statements' alike) is queued as it is issued, and an `s_waitcnt vmcnt(N)`
+    retires all but the N youngest -- an asm load is retired only when it is older than those N, so
+    a wait count too high for the loads it must cover is caught (their registers are then read while
+    still in flight).  lgkm loads are retired by any lgkmcnt wait in an asm statement and by a
+    compiler lgkmcnt(0) (the product's asm LDS reads wait in their own statement, form (i))."""
     lines = open(path).read().splitlines()
     bad = []
     pending = {}  # reg -> (kind, line of the load)
+    vmq = []      # vector-memory operations in issue order: the destination regs of asm loads, or None
     in_asm, block, block_start, func = False, [], 0, "?"
 
-    def retire(kind):
-        for r in [r for r, (k, _) in pending.items() if k == kind]:
+    def retire_lgkm():
+        for r in [r for r, (k, _) in pending.items() if k == "lgkm"]:
             del pending[r]
+
+    def wait_vm(n):
+        nonlocal vmq
+        old, vmq = (vmq, []) if n == 0 else (vmq[:-n], vmq[-n:])
+        for regs in old:
+            for r in regs or ():
+                if r in pending and pending[r][0] == "vm":
+                    del pending[r]
+
+    def waits_in(text):
+        for kind, n in _WAIT_CNT.findall(text):
+            if kind == "vmcnt":
+                wait_vm(int(n))
+            elif kind == "lgkmcnt":
+                yield int(n)
 
     for no, raw in enumerate(lines, 1):
         ln = raw.split(";")[0].strip() if not raw.strip().startswith(";;#ASM") else raw.strip()
@@ -229,19 +260,13 @@ def audit_asm(path: str):
         if raw.strip() == ";;#ASMEND":
             in_asm = False
             insts = [b for b in block if b and not b.startswith(";")]
-            waits = [b for b in insts if b.startswith("s_waitcnt")]
             loads = [b for b in insts if _LOAD_MN.match(b.split()[0]) and "lds" not in b.split()[0]
                      and not b.split()[0].endswith("_lds")]
-            if waits:
-                for w in waits:
-                    if "vmcnt" in w:
-                        retire("vm")
-                    if "lgkmcnt" in w:
-                        retire("lgkm")
-                continue
             touched = set()
             for b in insts:
                 mn, _, ops = b.partition(" ")
+                if mn == "s_waitcnt":
+                    continue
                 if b in loads:
                     dst, _, rest = ops.partition(",")
                     touched |= _regs(rest)
@@ -251,11 +276,20 @@ def audit_asm(path: str):
             if hit:
                 bad.append(f"{path}:{block_start} ({func}): asm statement reads v{sorted(hit)} while the "
                            f"load at line {pending[min(hit)][1]} is in flight")
-            for b in loads:
+            for b in insts:
                 mn, _, ops = b.partition(" ")
-                dst = ops.partition(",")[0]
-                for r in _regs(dst):
-                    pending[r] = (_kind(mn), no)
+                if mn == "s_waitcnt":
+                    if list(waits_in(ops)):
+                        retire_lgkm()
+                    continue
+                if b in loads:
+                    regs = _regs(ops.partition(",")[0])
+                    for r in regs:
+                        pending[r] = (_kind(mn), no)
+                    if _kind(mn) == "vm":
+                        vmq.append(regs)
+                elif _VMEM_MN.match(mn):
+                    vmq.append(None)
             continue
         if in_asm:
             block.append(raw.strip())
@@ -267,20 +301,23 @@ def audit_asm(path: str):
                     bad.append(f"{path}:{no} ({func}): function ends with asm loads never retired "
                                f"(lines {sorted({v[1] for v in pending.values()})})")
                 pending.clear()
+                vmq = []
                 if ln.endswith(":") and not ln.startswith("."):
                     func = ln[:-1]
             continue
         mn, _, ops = ln.partition(" ")
         if mn == "s_waitcnt":
-            if "vmcnt(0)" in ops:
-                retire("vm")
-            if "lgkmcnt(0)" in ops:
-                retire("lgkm")
+            if 0 in list(waits_in(ops)):
+                retire_lgkm()
             continue
         hit = _regs(ops) & set(pending)
         if hit:
             bad.append(f"{path}:{no} ({func}): compiler instruction '{ln}' touches v{sorted(hit)} while the "
                        f"asm load at line {pending[min(hit)][1]} is in flight")
+        if _VMEM_MN.match(mn):
+            vmq.append(None)
+            if len(vmq) > 256 and not any(vmq[:-64]):
+                vmq = vmq[-64:]  # vmcnt counts at most 63
     return bad
 
 

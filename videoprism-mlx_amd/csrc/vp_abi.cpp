@@ -174,10 +174,11 @@ int vp_finalize(vp_handle* h) {
   }
   const bool fold = is_bf16(h);
   if ((rc = pack_stack(h, px + "spatial_encoder/transformers_stack/x_layers/", c.num_spatial_layers, D, c.mlp_dim,
-                       c.num_heads, fold, h->spatial)))
+                       c.num_heads, fold, h->spatial, QKV_BLOCKED)))
     return rc;
   if ((rc = pack_stack(h, px + "temporal_encoder/transformers_stack/x_layers/", c.num_temporal_layers, D,
-                       c.mlp_dim, c.num_heads, fold, h->temporal, /*qk_perm*/ fold && c.model_dim == c.num_heads * 64)))
+                       c.mlp_dim, c.num_heads, fold, h->temporal,
+                       fold && c.model_dim == c.num_heads * 64 ? QKV_PER_HEAD : QKV_PLAIN)))
     return rc;
   std::vector<float> g(D);
   const char* lns[2] = {"spatial_ln", "temporal_ln"};

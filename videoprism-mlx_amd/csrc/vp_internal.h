@@ -278,12 +278,21 @@ inline std::vector<float> fold_ln(std::vector<float>& w, std::vector<float>& b, 
   return c;
 }
 
+// extra copies of the folded q|k|v rows a stack's attention path reads (pack_stack)
+enum QkvExtra {
+  QKV_PLAIN = 0,    // row-major [3D][D] only (auxiliary / text stacks)
+  QKV_PER_HEAD = 1, // + [q_h | k_h] per head (temporal stacks: the fused temporal attention)
+  QKV_BLOCKED = 2,  // + the row-blocked copy (spatial stacks: EPI_BF16_LN_BLK -> attn_spatial<.., true>)
+};
+
 // one scanned stack `pre` (".../x_layers/") -> L packed layers.  fold: LayerNorms folded into
 // the consuming GEMMs (bf16 handles, EPI_*_LN); otherwise W / b are the plain projections and the
-// LayerNorms run as kernels (ln*_g / ln*_b).
+// LayerNorms run as kernels (ln*_g / ln*_b).  The row-major q|k|v copy is always kept: it serves the
+// unfused attention paths (other patch grids, frame paddings, caps outside the fast range).
 template <class H>
 int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH, bool fold,
-               std::vector<LayerW>& out, bool qk_perm = false) {
+               std::vector<LayerW>& out, QkvExtra extra = QKV_PLAIN) {
+  const bool qk_perm = extra == QKV_PER_HEAD;
   const float qscale = 1.0f / std::sqrt((float)(D / NH));  // layers.py:576-583
   const auto& lng = param_data(h, pre + "layer_norm/scale");
   const auto& lnb = param_data(h, pre + "layer_norm/bias");
@@ -324,7 +333,7 @@ int pack_stack(H* h, const std::string& pre, int L, int64_t D, int64_t F, int NH
     if (fold) {
       const std::vector<float> c = fold_ln(t, tb, g1, be1, 3 * D, D);
       if ((rc = upload_f32(h, c, &lw.cqkv))) return rc;
-      if (!qk_perm && (3 * D) % 256 == 0) {  // the row-blocked copy (LayerW::wqkv_blk)
+      if (extra == QKV_BLOCKED && (3 * D) % 256 == 0) {  // the row-blocked copy (LayerW::wqkv_blk)
         const int64_t N3 = 3 * D;
         std::vector<float> pt((size_t)N3 * D), pb(N3), pc(N3);
         for (int64_t r = 0; r < N3; ++r) {
