@@ -100,9 +100,12 @@ def test_misaligned_frames_take_the_patchify_path(cuda):
     assert torch.equal(outs["bf16"], outs["f32"]) and torch.equal(outs["bf16"], outs["u8"])
     ref, _ = orc.factorized_encoder(var["params"], f32n.reshape(shape), cfg, "f64")
     got = outs["bf16"].double().cpu().numpy()
+    fused = aligned.double().cpu().numpy()
     pool_err = np.abs(_pooled(got) - _pooled(ref)).max()
-    d = (outs["bf16"].double() - aligned.double()).abs()
-    print(f"misaligned frames: pooled {pool_err:.3e} vs oracle; vs the aligned fused forward max {float(d.max()):.3e} "
-          f"mean {float(d.mean()):.3e}")
+    mean_err, mean_fused = np.abs(got - ref).mean(), np.abs(fused - ref).mean()
+    print(f"misaligned frames: pooled {pool_err:.3e} vs oracle; token mean-abs {mean_err:.3e} (aligned, fused "
+          f"patch embedding: {mean_fused:.3e})")
+    # the two patch embeddings differ only in their fp32 summation order (test_gpu_kernels.py
+    # test_patch_embed_fused_from_frames): both forwards are equally close to fp64
     assert pool_err < 1e-3
-    assert float(d.mean()) < 2e-3
+    assert mean_err <= 1.1 * mean_fused

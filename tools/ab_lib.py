@@ -73,5 +73,47 @@ def tattn(other):
     print("tattn:", " | ".join(f"{k} {min(v)*1e3:7.1f} us" for k, v in res.items()), flush=True)
 
 
+def spatial(other):
+    """The spatial attention (S = 256, 12 heads, 512 frames: the bench shape) over the row-major
+    q|k|v (vp_op_attention) and the row-blocked one (vp_dev_attention_spatial_blk), plus a padded
+    batch (the masked kernel) and an item count that is not a multiple of the grid: bitwise this vs
+    other, interleaved timing."""
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    H, D = 12, 768
+    libs = {"this": nat.load(), "other": ctypes.CDLL(other)}
+    for lib in libs.values():
+        for name in ("vp_op_attention", "vp_dev_attention_spatial_blk"):
+            f = getattr(lib, name)
+            f.restype, f.argtypes = nat._SIGNATURES[name]
+    st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    for nseq, blk, padded in ((512, True, False), (512, False, False), (37, True, False), (100, True, False), (16, False, True)):
+        qkv = torch.randn((nseq * 256, 3 * D), generator=g, device=dev)
+        qkv[:, :D] *= 0.125
+        qkv = qkv.to(torch.bfloat16)
+        pad = None
+        if padded:
+            pad = torch.zeros(nseq * 256, device=dev)
+            pad[5 * 256 + 200: 6 * 256] = 1.0
+        outs = {k: torch.empty((nseq * 256, D), device=dev, dtype=torch.bfloat16) for k in libs}
+
+        def run(k):
+            if blk:
+                assert libs[k].vp_dev_attention_spatial_blk(ptr(qkv), ptr(outs[k]), nseq, H, 50.0, ptr(pad), st()) == 0
+            else:
+                assert libs[k].vp_op_attention(1, ptr(qkv), ptr(outs[k]), nseq, 256, H, 50.0, ptr(pad), st()) == 0
+        for k in libs:
+            run(k)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(outs["this"], outs["other"]))
+        res = {k: [] for k in libs}
+        for _ in range(5):
+            for k in libs:
+                res[k].append(timeit(lambda k=k: run(k)))
+        print(f"spatial nseq={nseq} blk={blk} padded={padded}: bitwise this == other {same}; " + " | ".join(
+            f"{k} {min(v)*1e3:7.1f} us" for k, v in res.items()), flush=True)
+
+
 if __name__ == "__main__":
-    {"tattn": tattn}[sys.argv[1]](sys.argv[2])
+    {"tattn": tattn, "spatial": spatial}[sys.argv[1]](sys.argv[2])

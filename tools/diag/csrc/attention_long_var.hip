@@ -1,8 +1,8 @@
 // A/B builds of the auxiliary (4096-token) attention kernel (videoprism-mlx_amd/csrc/
 // attention_long_kernel.h) for the tools' diag library: var 0 = the product kernel, 1 = the
 // polynomial numerator in scalar instead of packed fp32 (bitwise the same output), 2 = without the
-// quadratic tier for small logits, 4 = the row sum one value at a time (bits combine: 6 = round 3's
-// kernel, 7).
+// quadratic tier for small logits, 4 = the row sum one value at a time, 8 = without the linear tier
+// (round 4's product kernel) (bits combine: 6 = round 3's kernel, 7).
 #include "attention_long_kernel.h"
 
 extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int64_t num_seq, int64_t S,
@@ -15,6 +15,7 @@ extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int6
   if (var == 2) e = launch_attn_long<2>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 4) e = launch_attn_long<4>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 6) e = launch_attn_long<6>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 8) e = launch_attn_long<8>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 7) e = launch_attn_long<7>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   return e == hipSuccess ? 0 : -1;
 }

@@ -27,12 +27,13 @@ constexpr int kLgStages = 4;
 constexpr int kLgStageBytes = 2 * kLgChunk * 128;  // K then V, 128 B per key row
 constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 
-// The numerator takes the quadratic tier on tiles whose logits all satisfy |x| <= 0.24 cap (vp_common.h
-// capped_exp16 QUAD: as accurate as the cubic) and the row sum accumulates in packed pairs; with logits
-// of std 0.5 / 6 (tools/attn_bench.py long, LvT-Large shape) 2.606 / 2.926 ms vs 2.828 / 2.953 without
-// either.  VAR (A/B builds of the diag library; the product uses 0): 1 = the polynomial numerator in
-// scalar instead of packed fp32 arithmetic (bitwise the same values); 2 = no quadratic tier; 4 = the
-// row sum one value at a time
+// The numerator takes the linear tier on tiles whose logits all satisfy |x| <= 0.10 cap (vp_common.h
+// capped_exp16 LIN), else the quadratic tier for |x| <= 0.24 cap (QUAD: as accurate as the cubic), and
+// the row sum accumulates in packed pairs; with logits of std 0.5 / 6 (tools/attn_bench.py long,
+// LvT-Large shape) 2.606 / 2.926 ms vs 2.828 / 2.953 without the quadratic tier and the packed sum.
+// VAR (A/B builds of the diag library; the product uses 0): 1 = the polynomial numerator in scalar
+// instead of packed fp32 arithmetic (bitwise the same values); 2 = no quadratic tier; 4 = the row sum
+// one value at a time; 8 = no linear tier
 template <int VAR = 0>
 __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* __restrict__ qkv,
                                                                   bf16_t* __restrict__ o, int S,
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
-      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0>(x, p, c1, c2, cp);
+      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0>(x, p, c1, c2, cp);
       if constexpr ((VAR & 4) == 0) {  // row sum in packed pairs
 #pragma unroll
         for (int i = 0; i < 16; i += 2) lsum2 += f2_t{p[i], p[i + 1]};

@@ -71,29 +71,38 @@ __device__ __forceinline__ float capped_exp_exact(float x, float two_log2e_over_
 // holding a larger logit take the exact path (wave-uniform branch).
 // QUAD tier (tiles whose logits all satisfy |x| <= 0.24 cap): T fitted by a quadratic on v in
 // [0, 0.24^2] (relative error 3.5e-7, tools/fit_gelu.py fit_tanh(0.24, 2)), coefficients q0..q2.
+// LIN tier (tiles whose logits all satisfy |x| <= 0.10 cap): T fitted by a line on v in [0, 0.10^2]
+// (relative error 1.7e-6, tools/fit_gelu.py fit_tanh(0.10, 1): exponent error <= 1.2e-5, 0.3 % of a
+// bf16 ulp of the numerator), coefficients l0, l1 -- three VALU operations per logit instead of four.
 struct CapPoly {
   float k0, k1, k2, k3, x0;
   float q0, q1, q2, x1;
+  float l0, l1, x2;
 };
 
 inline CapPoly make_cap_poly(float cap) {
   const double t[4] = {0.9999995827674866, -0.33327752351760864, 0.1321016252040863, -0.045063190162181854};
   const double u[3] = {0.9999996877028773, -0.33323595618512314, 0.12879159575308177};
+  const double w[2] = {0.9999983358095185, -0.33200482774291656};
   const double l2e = 1.4426950408889634, c2 = (double)cap * cap;
   return CapPoly{(float)(l2e * t[0]), (float)(l2e * t[1] / c2), (float)(l2e * t[2] / (c2 * c2)),
                  (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap,
-                 (float)(l2e * u[0]), (float)(l2e * u[1] / c2), (float)(l2e * u[2] / (c2 * c2)), 0.24f * cap};
+                 (float)(l2e * u[0]), (float)(l2e * u[1] / c2), (float)(l2e * u[2] / (c2 * c2)), 0.24f * cap,
+                 (float)(l2e * w[0]), (float)(l2e * w[1] / c2), 0.10f * cap};
 }
 
 // PACKED: the polynomial in pairs of packed fp32 (v_pk_mul_f32 / v_pk_fma_f32), else scalar fp32
 // (the same IEEE operations per value, so bitwise the same result; packed fp32 VALU beside another
 // wave's MFMAs is priced as an anti-lever in MI355X_MICROARCH.md's price list)
-template <bool PACKED = true, bool QUAD = false>
+template <bool PACKED = true, bool QUAD = false, bool LIN = false>
 __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
   float mx = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
-  if (QUAD && __builtin_amdgcn_ballot_w64(mx > cp.x1) == 0) {
+  if (LIN && __builtin_amdgcn_ballot_w64(mx > cp.x2) == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = __builtin_amdgcn_exp2f(x[i] * fmaf(cp.l1, x[i] * x[i], cp.l0));
+  } else if (QUAD && __builtin_amdgcn_ballot_w64(mx > cp.x1) == 0) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const float u = x[i] * x[i];
