@@ -225,7 +225,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
   chunk_ready(std::integral_constant<int, 0>{});
   // (a software-pipelined form -- the S^T MFMAs of tile kt+1 issued ahead of tile kt's
   // numerators -- is bitwise equal but measured 289.8 vs 206.8 us: at 128 VGPRs it spills inside
-  // the loop)
+  // the loop; profiles/HISTORY.md round 3)
 #pragma unroll 1
   for (int cc = 0; cc < 4; ++cc) {
     if (cc == 1) chunk_ready(std::integral_constant<int, 1>{});

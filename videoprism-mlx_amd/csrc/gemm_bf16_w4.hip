@@ -30,7 +30,7 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
   // Every configuration stores its output nontemporally: +1.7 % on the whole forward vs plain stores
   // (same device, back-to-back: 947.8 vs 931.7 clips/s); plain stores on the residual-stream producers
   // (x in the Infinity Cache for the next GEMM) and on the q|k|v projection (for the spatial attention)
-  // measured no faster.
+  // measured no faster (profiles/HISTORY.md).
   constexpr bool S3 = true, S2 = false;
   // the S3 residual epilogues peel their last K-tile (gemm_w4_kernel.h kEarly: K >= 2 BK); the
   // other bf16-residual epilogues take S3 only for K >= 2048

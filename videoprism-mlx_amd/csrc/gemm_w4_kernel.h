@@ -92,7 +92,7 @@ __device__ __forceinline__ bf16x4 w4_tr_read(const char* p) {
 
 // the LN fold of 4 accumulator values (r * a + (m * c + b)) in packed pairs: two IEEE fmas per value
 // (the scalar form is bitwise equal and measured no faster beside the fused epilogues' MFMAs:
-// QK launch 250.9 vs 246.5 us, V launch 161.8 vs 159.0)
+// QK launch 250.9 vs 246.5 us, V launch 161.8 vs 159.0, profiles/HISTORY.md)
 __device__ __forceinline__ void fold4(const f32x4& a, float r, float m, const float4& c, const float4& b, f32x2_t& lo,
                                       f32x2_t& hi) {
   const f32x2_t rr = f32x2_t(r), mm = f32x2_t(m);
