@@ -197,3 +197,29 @@ def test_prepare_frames_contract(cuda):
         assert err <= 1e-5, err
     finally:
         lib.vp_destroy(h)
+
+
+def test_long_clip_batch_chunks_bitwise(cuda):
+    """vp_forward's chunking scales with T: at T = 64 a chunk holds 42 clips (the FFN hidden of 43 would
+    pass the GEMM's 32-bit operand range), so B = 43 runs as 42 + 1.  Base bf16, full depth: clips on both
+    sides of the chunk boundary equal their B = 1 runs bit for bit."""
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    var = params.synthetic_params(cfg, seed=4)
+    mdl = models.get_model("videoprism_public_v1_base", fprop_dtype=torch.bfloat16)
+    eng = mdl.engine(var, torch.cuda.current_device())
+    T = 64
+    sizes = {}
+    for b in (42, 43):
+        n = ctypes.c_size_t()
+        _native.call("vp_workspace_bytes", eng._h, b, T, 288, 288, ctypes.byref(n))
+        sizes[b] = n.value
+    assert sizes[42] == sizes[43]  # one chunk of 42 clips
+    gen = torch.Generator(device=cuda).manual_seed(8)
+    batch = torch.rand((43, T, 288, 288, 3), generator=gen, device=cuda).to(torch.bfloat16)
+    full, _ = mdl.apply(var, batch)
+    assert full.shape == (43, T * 256, 768)
+    full = full.clone()
+    for b in (0, 41, 42):
+        one, _ = mdl.apply(var, batch[b:b + 1].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(one[0], full[b]), b

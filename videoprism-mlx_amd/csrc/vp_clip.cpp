@@ -490,6 +490,8 @@ int vp_clip_encode_text(vp_clip* c, const int32_t* ids, const float* paddings, i
   f.xs_f32 = true;
   f.hb = ws + w.hb; f.big = ws + w.big;
   f.pf = &c->video->prof;
+  f.cls_all = PC_ATTN_TEXT;  // the whole text tower in one profiler class ("text_tower"), so the vision GEMM
+                             // classes (and bench.py's dominant-kernel roofline) hold the vision launches only
   int rc = f.run_stack(c->text, x, (int)Q, (int)L + 1, pad, 4 * D, PC_ATTN_TEXT, ATT_TEXT, false, true);
   if (rc) return rc;
   // unimodal_ln on the CLS rows, then L2 (encoders.py:752-758, :905-908)

@@ -118,7 +118,7 @@ enum ProfClass {
 };
 inline const char* kProfNames[PC_COUNT] = {"patchify", "gemm_patch_embed", "layernorm", "gemm_qkv",
                                     "attention_spatial", "attention_temporal", "gemm_post",
-                                    "gemm_ffn1_gelu", "gemm_ffn2", "attention_aux", "attention_text",
+                                    "gemm_ffn1_gelu", "gemm_ffn2", "attention_aux", "text_tower",
                                     "pooler", "misc", "gemm_qkv_temporal_attn"};
 
 // HIP-event profiler: start/stop events around each launch on the launch stream.
@@ -525,10 +525,12 @@ struct Fwd {
   float* st_part = nullptr;  // [D/128][M][2] partial row statistics (folded LayerNorm)
   float* ln_rs = nullptr;    // [M][2] (rstd, -mean*rstd)
   Profiler* pf = nullptr;
+  int cls_all = -1;          // >= 0: every launch of this context counts in that class (the text tower)
 
   // profiled launch: records events around `fn` when vp_profile_enable() is active
   template <class Fn>
   hipError_t rec(int cls, double flops, double bytes, Fn&& fn) {
+    if (cls_all >= 0) cls = cls_all;
     auto launch = [&]() {
       vp::g_last_kernel = nullptr;
       const hipError_t e = fn();
