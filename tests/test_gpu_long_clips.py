@@ -223,3 +223,65 @@ def test_long_clip_batch_chunks_bitwise(cuda):
         one, _ = mdl.apply(var, batch[b:b + 1].contiguous())
         torch.cuda.synchronize()
         assert torch.equal(one[0], full[b]), b
+
+
+# --- one operand past the 4-wave GEMM's 32-bit buffer range (4 GiB): row ranges ---------------------------
+# rows of 3072 bf16 (6144 B): the range holds 698,880 rows (2730 x 256, also a multiple of 768)
+_RANGE_ROWS = 698880
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("epi", ["pos", "resid_ffn"])
+def test_gemm_operand_past_4gib_row_ranges(cuda, epi):
+    """A [700416, 3072] bf16 (4.30 GB) through vp_op_gemm: the launch splits at row 698,880.  Every row is
+    one tile's K-ordered sum, so the rows around the split equal a launch over just those rows, bit for
+    bit, with the row-indexed arguments (pos period 768, resid, rowpad) following the range."""
+    M, K, N = _RANGE_ROWS + 1536, 3072, 256
+    gen = torch.Generator(device=cuda).manual_seed(11)
+    a = torch.randn((M, K), generator=gen, device=cuda).to(torch.bfloat16)
+    w = (torch.randn((N, K), generator=gen, device=cuda) * K ** -0.5).to(torch.bfloat16)
+    b = torch.randn(N, generator=gen, device=cuda)
+    lo, hi = _RANGE_ROWS - 768, _RANGE_ROWS + 1536
+    if epi == "pos":
+        pos = torch.randn((768, N), generator=gen, device=cuda)
+        full = _native.op_gemm(a, w, b, _native.EPI_POS_BF16, pos=pos)
+        part = _native.op_gemm(a[lo:hi], w, b, _native.EPI_POS_BF16, pos=pos)
+        ref = (a[lo:hi].float() @ w.float().T + b + pos.repeat(3, 1))
+    else:
+        x = torch.randn((M, N), generator=gen, device=cuda).to(torch.bfloat16)
+        pad = (torch.rand(M, generator=gen, device=cuda) < 0.1).float()
+        full, part = x.clone(), x[lo:hi].clone()
+        _native.op_gemm(a, w, b, _native.EPI_RESID_FFN_BF16, out=full, resid=full, rowpad=pad)
+        _native.op_gemm(a[lo:hi], w, b, _native.EPI_RESID_FFN_BF16, out=part, resid=part, rowpad=pad[lo:hi])
+        ref = x[lo:hi].float() + (a[lo:hi].float() @ w.float().T + b) * (1 - pad[lo:hi, None])
+    torch.cuda.synchronize()
+    assert torch.equal(full[lo:hi], part)
+    err = (part.float() - ref).abs().max().item()
+    print(f"{epi}: rows {lo}..{hi} across the range split bitwise; max-abs vs fp32 {err:.3e}")
+    assert err <= 2 ** -7 * ref.abs().max().item()  # the bf16 output's rounding, with margin
+
+
+@pytest.mark.timeout(600)
+def test_single_clip_past_the_gemm_operand_range(cuda):
+    """One Base bf16 clip of 2736 frames: its FFN hidden activation (700,416 x 3072 bf16 = 4.30 GB) passes
+    the GEMM's 32-bit buffer range, so ffn_layer2 runs as two row ranges split at frame 2730 (previously
+    an ENOTSUP).  Spatial features depend on their own frame only (encoders.py:459-478), so frames on
+    both sides of the split equal a 16-frame clip of the same frames bit for bit; the temporal encoder
+    attends over 2736 frames (the unfused attention, any S) and the output stays finite."""
+    cfg = models.CONFIGS["videoprism_v1_base"]
+    var = params.synthetic_params(cfg, seed=12)
+    mdl = models.get_model("videoprism_public_v1_base", fprop_dtype=torch.bfloat16)
+    eng = mdl.engine(var, torch.cuda.current_device())
+    T = 2736
+    gen = torch.Generator(device=cuda).manual_seed(13)
+    video = torch.randint(0, 256, (1, T, 288, 288, 3), generator=gen, device=cuda, dtype=torch.uint8)
+    emb, sp = eng.forward(video, want_spatial=True)
+    torch.cuda.synchronize()
+    assert emb.shape == (1, T * 256, 768)
+    assert bool(torch.isfinite(emb).all()) and bool(torch.isfinite(sp).all())
+    sp = sp.view(T, 256, 768)
+    for f0 in (0, 2720):
+        _, one = eng.forward(video[:, f0:f0 + 16].contiguous(), want_spatial=True)
+        torch.cuda.synchronize()
+        assert torch.equal(one.view(16, 256, 768), sp[f0:f0 + 16]), f0
+    print(f"T={T}: spatial frames 0..15 and 2720..2735 bitwise equal to 16-frame clips")

@@ -311,12 +311,12 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
 }
 
 // Kernel choice for the forward and vp_op_gemm: the 4-wave kernel wherever its 32-bit buffer
-// offsets reach (the forward chunks its batch so that they always do), except the fp32-residual
+// offsets reach W (A past them runs in row ranges), except the fp32-residual
 // epilogues at K < 1024 (text tower), where the 8-wave kernel measured faster.
 hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                           int N, int K, const EpiArgs& ep, hipStream_t s) {
-  const bool w4_ok = (uint64_t)M * (uint64_t)lda * 2 < 0xFFFFFFF0ull &&
-                     (uint64_t)N * (uint64_t)ldw * 2 < 0xFFFFFFF0ull;
+  // (gemm_bf16_w4 walks an A past the 32-bit buffer range in row ranges; W must fit one range)
+  const bool w4_ok = (uint64_t)N * (uint64_t)ldw * 2 < 0xFFFFFFF0ull;
   if (epi >= EPI_BF16_LN) return w4_ok ? gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s) : hipErrorInvalidValue;
   if (w4_ok && !((epi == EPI_RESID_F32 || epi == EPI_RESID_FFN) && K < 1024))
     return gemm_bf16_w4(epi, A, lda, W, ldw, M, N, K, ep, s);

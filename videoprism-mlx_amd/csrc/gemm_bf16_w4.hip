@@ -1,6 +1,8 @@
 // Production instantiations and dispatch of the 4-wave bf16 GEMM (kernel template and design notes:
 // gemm_w4_kernel.h).  Only production configurations are compiled here; the ablation builds live
 // in the tools' diag library (tools/diag/csrc/gemm_w4_abl.hip).
+#include <algorithm>
+
 #include "gemm_w4_kernel.h"
 
 namespace vp {
@@ -21,9 +23,11 @@ int w4_ngrp(int M, int N, int K, int grid) {
   return g;
 }
 
-hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
-                        int N, int K, const EpiArgs& ep, hipStream_t s) {
-  // byte offsets into A / W must fit the 32-bit buffer range
+namespace {
+
+// one launch: the byte offsets into A / W must fit the 32-bit buffer range
+hipError_t gemm_bf16_w4_launch(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                               int N, int K, const EpiArgs& ep, hipStream_t s) {
   if ((uint64_t)M * (uint64_t)lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * (uint64_t)ldw * 2 >= 0xFFFFFFF0ull)
     return hipErrorInvalidValue;
   if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
@@ -89,16 +93,73 @@ hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, 
   return hipErrorInvalidValue;
 }
 
+}  // namespace
+
+// Rows are independent in every epilogue, so an A operand past the 32-bit buffer range (a long clip:
+// the FFN hidden of one 16 x 288 x 288 clip is 4096 x 3072 x 2 B = 24 MiB, 4 GiB at ~2730 frames) runs
+// as consecutive row ranges, each a launch whose row-indexed arguments start at its first row: out /
+// resid by rows (the row-blocked layouts too: a 16-row block row is N elements), ln_rs / rowpad /
+// st_part by rows (st_rows stays the full stride of the partial planes), the fused temporal
+// attention's P by 16-row sequences, pos unchanged (ranges are multiples of pos_rows).  Each output
+// element is still one tile's K-ordered sum: bitwise the single launch.
+hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
+                        int N, int K, const EpiArgs& ep, hipStream_t s) {
+  const uint64_t rowb = (uint64_t)lda * 2;
+  if (M <= 0 || (uint64_t)M * rowb < 0xFFFFFFF0ull) return gemm_bf16_w4_launch(epi, A, lda, W, ldw, M, N, K, ep, s);
+  const bool f32_io = epi == EPI_RESID_F32 || epi == EPI_RESID_FFN || epi == EPI_POS_F32;  // fp32 out / resid
+  const bool pos = epi == EPI_POS_F32 || epi == EPI_POS_BF16 || epi == EPI_POS_BF16_ST;
+  int64_t unit = BM;  // row ranges: multiples of the tile (and of the positional table's period)
+  if (pos) {
+    int64_t a = BM, b = ep.pos_rows > 0 ? ep.pos_rows : 1;
+    while (b) { const int64_t t = a % b; a = b; b = t; }
+    unit = (int64_t)BM / a * (ep.pos_rows > 0 ? ep.pos_rows : 1);
+  }
+  const int64_t max_rows = (int64_t)(0xFFFFFFF0ull / rowb) / unit * unit;
+  if (max_rows < unit) return hipErrorInvalidValue;
+  for (int64_t r0 = 0; r0 < M; r0 += max_rows) {
+    const int rows = (int)std::min<int64_t>(max_rows, M - r0);
+    const int64_t pel = (r0 / 16) * ep.heads * 256;  // fused temporal P: 16 x 16 bf16 per (sequence, head)
+    EpiArgs e = ep;
+    if (epi == EPI_QK_TATTN_LN) e.out = static_cast<bf16_t*>(ep.out) + pel;
+    else e.out = static_cast<char*>(ep.out) + r0 * ep.ldo * (f32_io ? 4 : 2);
+    if (ep.resid) {
+      if (epi == EPI_V_TATTN_LN) e.resid = static_cast<const bf16_t*>(ep.resid) + pel;
+      else e.resid = static_cast<const char*>(ep.resid) + r0 * ep.ldr * (f32_io ? 4 : 2);
+    }
+    if (ep.rowpad) e.rowpad = ep.rowpad + r0;
+    if (ep.ln_rs) e.ln_rs = ep.ln_rs + 2 * r0;
+    if (ep.st_part) e.st_part = ep.st_part + 2 * r0;  // st_rows: the full stride of the partial planes
+    const hipError_t err = gemm_bf16_w4_launch(epi, A + r0 * lda, lda, W, ldw, rows, N, K, e, s);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
 hipError_t gemm_bf16_w4_video(int epi, const bf16_t* video, int P, const bf16_t* W, int M, int N, const EpiArgs& ep,
                               hipStream_t s) {
   if (!video_patch_ok(P) || M % BM || N % BN) return hipErrorInvalidValue;
   const int64_t lda = 16LL * P * 3;  // elements of one pixel row
   const int K = video_patch_k(P);
-  if ((uint64_t)(M / BM) * 16 * P * lda * 2 >= 0xFFFFFFF0ull || (uint64_t)N * K * 2 >= 0xFFFFFFF0ull)
+  if ((uint64_t)N * K * 2 >= 0xFFFFFFF0ull || (epi != EPI_POS_BF16_ST && epi != EPI_POS_BF16) || ep.pos_rows != 256)
     return hipErrorInvalidValue;
-  if (epi == EPI_POS_BF16_ST) return launch_w4<EPI_POS_BF16_ST, false, false, 0, true>(video, lda, W, K, M, N, K, ep, s);
-  if (epi == EPI_POS_BF16) return launch_w4<EPI_POS_BF16, false, false, 0, true>(video, lda, W, K, M, N, K, ep, s);
-  return hipErrorInvalidValue;
+  // one frame = 16 P pixel rows = one 256-row tile; frames past the 32-bit buffer range run as consecutive
+  // frame ranges (rows independent, the position table's period is the frame: bitwise one launch)
+  const int64_t frame_elems = 16LL * P * lda;
+  const int64_t max_frames = (int64_t)(0xFFFFFFF0ull / (uint64_t)(frame_elems * 2));
+  const int64_t frames = M / BM;
+  for (int64_t f0 = 0; f0 < frames; f0 += max_frames) {
+    const int rows = (int)(std::min<int64_t>(max_frames, frames - f0) * BM);
+    const int64_t r0 = f0 * BM;
+    EpiArgs e = ep;
+    e.out = static_cast<bf16_t*>(ep.out) + r0 * ep.ldo;
+    if (ep.st_part) e.st_part = ep.st_part + 2 * r0;
+    const bf16_t* v = video + f0 * frame_elems;
+    const hipError_t err = epi == EPI_POS_BF16_ST
+                               ? launch_w4<EPI_POS_BF16_ST, false, false, 0, true>(v, lda, W, K, rows, N, K, e, s)
+                               : launch_w4<EPI_POS_BF16, false, false, 0, true>(v, lda, W, K, rows, N, K, e, s);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
 }
 
 }  // namespace vp

@@ -261,8 +261,8 @@ int vp_workspace_bytes(const vp_handle* h, int64_t B, int64_t T, int64_t H, int6
 
 namespace {
 
-// FactorizedEncoder.__call__ over one chunk of B clips (B <= chunk_clips, so every GEMM operand
-// fits the 32-bit buffer range); vp_forward below walks the batch chunk by chunk
+// FactorizedEncoder.__call__ over one chunk of B clips (B <= chunk_clips: a workspace of about 4 GiB of
+// FFN hidden activation); vp_forward below walks the batch chunk by chunk
 int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int64_t T, int64_t H,
                   int64_t W, const float* frame_paddings, void* out, int out_dtype,
                   void* spatial_out, void* workspace, void* stream) {

@@ -433,7 +433,7 @@ int vp_clip_encode_video(vp_clip* c, const void* video, int in_dtype, int64_t B,
   int rc = vp_clip_video_workspace_bytes(c, B, T, H, W, &need);
   if (rc) return rc;
   if (ws_bytes < need) return fail(VP_EINVAL, "workspace too small: need " + std::to_string(need));
-  // the batch in chunks of independent clips (each chunk's GEMM operands within 4 GiB)
+  // the batch in chunks of independent clips (vp_internal.h chunk_clips)
   const int64_t Bc = chunk_of(c->video, B, T, H, W);
   const vp_config& v = c->cfg.video;
   const int64_t N = (H / v.patch_size) * (W / v.patch_size), D = v.model_dim;

@@ -442,18 +442,18 @@ inline WsLayout ws_layout(const vp_handle* h, int64_t B, int64_t T, int64_t H, i
   return L;
 }
 
-// Clips per forward chunk.  The bf16 GEMM stages its A operand through a buffer descriptor with
-// 32-bit byte offsets, so every GEMM's padded rows x lda x 2 B must stay below 4 GiB (the widest A
-// is the FFN hidden activation, lda = mlp_dim).  The forward entry points process any B as
-// consecutive chunks of at most this many clips (clips are independent, encoders.py:411-580), each
-// in the same workspace.  0: a single clip is already too large.
+// Clips per forward chunk: the forward entry points process any B as consecutive chunks of at most this
+// many clips (clips are independent, encoders.py:411-580), each in the same workspace, which bounds the
+// workspace at about 4 GiB of FFN hidden activation (170 clips of 16 x 288 x 288).  A single clip always
+// fits a chunk: the GEMMs walk an operand past the 32-bit buffer range in row ranges (gemm_bf16_w4.hip),
+// so clip length is bounded by device memory only.
 inline int64_t chunk_clips(const vp_config& c, int64_t T, int64_t H, int64_t W) {
   const int64_t P = c.patch_size;
   const int64_t tok = T * (H / P) * (W / P);
   const int64_t kpad = ((P * P * 3 + 63) / 64) * 64;
   const int64_t lda = std::max<int64_t>(std::max<int64_t>(c.model_dim, c.mlp_dim), kpad);
   const int64_t max_rows = (int64_t)(0xFFFFFFF0ull / (uint64_t)(2 * lda)) / 256 * 256;
-  return tok > 0 ? max_rows / tok : 0;
+  return tok > 0 ? std::max<int64_t>(1, max_rows / tok) : 1;
 }
 
 inline int check_geometry(const vp_handle* h, int64_t B, int64_t T, int64_t H, int64_t W) {
@@ -463,9 +463,9 @@ inline int check_geometry(const vp_handle* h, int64_t B, int64_t T, int64_t H, i
   if (H % P || W % P)
     return fail(VP_EINVAL, "Image height (" + std::to_string(H) + ") and width (" + std::to_string(W) +
                                ") should be multiples of patch_size (" + std::to_string(P) + ").");
-  if (chunk_clips(h->cfg, T, H, W) < 1)
-    return fail(VP_ENOTSUP, "one clip of " + std::to_string(T) + "x" + std::to_string(H) + "x" + std::to_string(W) +
-                                " exceeds the GEMM operand range (4 GiB per operand)");
+  if (T * (H / P) * (W / P) > ((int64_t)1 << 30))
+    return fail(VP_EINVAL, "one clip of " + std::to_string(T) + "x" + std::to_string(H) + "x" + std::to_string(W) +
+                               " has more than 2^30 tokens (32-bit row indices)");
   return VP_OK;
 }
 

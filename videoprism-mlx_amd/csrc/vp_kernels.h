@@ -91,7 +91,8 @@ hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int
                      int N, int K, const EpiArgs& ep, hipStream_t s);
 
 // 4-wave (one wave per SIMD, 128x128 per wave, 16x16x32 MFMA, full-line buffer_load..lds
-// staging) decomposition; needs M*lda*2 and N*ldw*2 < 4 GiB (32-bit buffer offsets)
+// staging) decomposition; needs N*ldw*2 < 4 GiB (32-bit buffer offsets); an A operand past that range
+// runs as consecutive row ranges (gemm_bf16_w4.hip)
 hipError_t gemm_bf16_w4(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                         int N, int K, const EpiArgs& ep, hipStream_t s);
 // patch embedding straight from bf16 frames (no patch tensor): video [M/256 frames]
