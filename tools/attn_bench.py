@@ -56,16 +56,16 @@ def main():
 
 def long_variants():
     """The auxiliary (4096-token) attention at the LvT-Large bench shape (32 clips x 16 heads, S = 4096):
-    the product kernel (var 0) against its diag-library A/B builds (1: scalar polynomial numerator,
-    2: without the quadratic tier for tiles with |logit| <= 0.24 cap, 4: scalar row sum, 8: without the
-    linear tier for |logit| <= 0.10 cap = round 4's kernel; 6 = round 3's kernel), at two
-    logit scales (std 0.5: every tile in the quadratic tier; std 6: mixed tiers), interleaved rounds.
+    the product kernel (var 0) against its diag-library A/B builds (attention_long_kernel.h VAR bits:
+    8: without the linear tier for |logit| <= 0.10 cap = round 4's kernel; 16: row sum on the MFMA;
+    32: row sum by v_dot2_f32_bf16; 64: unpaired scalar numerator and row sum; 80, 96 combined), at three
+    logit scales (std 0.5 / 2 / 6: linear, quadratic / cubic and mixed tiers), interleaved rounds.
     VP_DIAG_LIB=1 python tools/attn_bench.py long"""
     dev = torch.device("cuda:0")
     nseq, heads, S = 32, 16, 4096
     D = heads * 64
     st = lambda: torch.cuda.current_stream().cuda_stream
-    variants = (0, 8, 1, 2, 4, 6)
+    variants = (0, 8, 16, 32, 64, 80, 96)
     for qscale in (0.0625, 0.25, 0.75):
         g = torch.Generator(device=dev).manual_seed(0)
         qkv = torch.randn((nseq * S, 3 * D), generator=g, device=dev)

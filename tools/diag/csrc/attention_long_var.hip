@@ -2,7 +2,8 @@
 // attention_long_kernel.h) for the tools' diag library: var 0 = the product kernel, 1 = the
 // polynomial numerator in scalar instead of packed fp32 (bitwise the same output), 2 = without the
 // quadratic tier for small logits, 4 = the row sum one value at a time, 8 = without the linear tier
-// (round 4's product kernel) (bits combine: 6 = round 3's kernel, 7).
+// (round 4's product kernel), 16 = the row sum on the MFMA, 32 = the row sum by v_dot2_f32_bf16,
+// 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32 (bits combine: 6 = round 3's kernel).
 #include "attention_long_kernel.h"
 
 extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int64_t num_seq, int64_t S,
@@ -16,6 +17,11 @@ extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int6
   if (var == 4) e = launch_attn_long<4>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 6) e = launch_attn_long<6>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 8) e = launch_attn_long<8>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 16) e = launch_attn_long<16>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 32) e = launch_attn_long<32>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 64) e = launch_attn_long<64>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 80) e = launch_attn_long<80>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 96) e = launch_attn_long<96>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 7) e = launch_attn_long<7>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   return e == hipSuccess ? 0 : -1;
 }

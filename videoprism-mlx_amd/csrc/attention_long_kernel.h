@@ -33,9 +33,11 @@ constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 // LvT-Large shape) 2.606 / 2.926 ms vs 2.828 / 2.953 without the quadratic tier and the packed sum.
 // VAR (A/B builds of the diag library; the product uses 0): 1 = the polynomial numerator in scalar
 // instead of packed fp32 arithmetic (bitwise the same values); 2 = no quadratic tier; 4 = the row sum
-// one value at a time; 8 = no linear tier
+// one value at a time; 8 = no linear tier; 16 = the row sum on the MFMA (a ones A operand against the
+// bf16 numerators, so the sum of the rounded values P.V uses); 32 = the row sum by v_dot2_f32_bf16 of
+// the bf16 numerator pairs; 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32
 template <int VAR = 0>
-__global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* __restrict__ qkv,
                                                                   bf16_t* __restrict__ o, int S,
                                                                   int heads, int nqb, float cap,
                                                                   int xcd_map, CapPoly cp) {
@@ -90,6 +92,7 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
   const float c1 = 2.0f * kLog2e / cap;
   const float c2 = cap * kLog2e;
   f32x16 y0 = {}, y1 = {};
+  [[maybe_unused]] f32x16 ysum = {};
   float lsum = 0.0f;
   typedef float f2_t __attribute__((ext_vector_type(2)));
   f2_t lsum2 = {0.0f, 0.0f};
@@ -130,8 +133,17 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
-      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0>(x, p, c1, c2, cp);
-      if constexpr ((VAR & 4) == 0) {  // row sum in packed pairs
+      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0, (VAR & 64) != 0>(x, p, c1, c2, cp);
+      if constexpr ((VAR & 48) != 0) {
+        // row sum from the bf16 numerators below
+      } else if constexpr ((VAR & 64) != 0) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          float t;
+          asm("v_add_f32 %0, %1, %2" : "=v"(t) : "v"(p[i]), "v"(p[i + 1]));
+          asm("v_add_f32 %0, %1, %2" : "=v"(lsum) : "v"(lsum), "v"(t));
+        }
+      } else if constexpr ((VAR & 4) == 0) {  // row sum in packed pairs
 #pragma unroll
         for (int i = 0; i < 16; i += 2) lsum2 += f2_t{p[i], p[i + 1]};
       } else {
@@ -145,6 +157,16 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
 #pragma unroll
         for (int j = 0; j < 4; ++j) u[j] = pack_bf16x2(p[8 * s + 2 * j], p[8 * s + 2 * j + 1]);
         pf[s] = *reinterpret_cast<bf16x8*>(u);
+        if constexpr ((VAR & 32) != 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            asm("v_dot2_f32_bf16 %0, %1, %2, %3" : "=v"(lsum) : "v"(u[j]), "v"(0x3f803f80u), "v"(lsum));
+        }
+      }
+      if constexpr ((VAR & 16) != 0) {
+        const bf16x8 ones = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+        ysum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[0], ysum, 0, 0, 0);
+        ysum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[1], ysum, 0, 0, 0);
       }
       uint32_t vad[2][2];
 #pragma unroll
@@ -172,8 +194,12 @@ __global__ __launch_bounds__(kLgThreads, 2) void attn_long_kernel(const bf16_t* 
       }
     }
   }
-  if constexpr ((VAR & 4) == 0) lsum = lsum2.x + lsum2.y;
-  lsum += __shfl_xor(lsum, 32);
+  if constexpr ((VAR & 16) != 0) {
+    lsum = ysum[0];  // every row of the ones product holds the full sum of its query column
+  } else {
+    if constexpr ((VAR & 100) == 0) lsum = lsum2.x + lsum2.y;
+    lsum += __shfl_xor(lsum, 32);
+  }
   const float inv = 1.0f / lsum;
   bf16_t* op = o + ((int64_t)seq * S + q0 + (lane & 31)) * D + h * 64 + 4 * half;
 #pragma unroll

@@ -94,20 +94,41 @@ inline CapPoly make_cap_poly(float cap) {
 // PACKED: the polynomial in pairs of packed fp32 (v_pk_mul_f32 / v_pk_fma_f32), else scalar fp32
 // (the same IEEE operations per value, so bitwise the same result; packed fp32 VALU beside another
 // wave's MFMAs is priced as an anti-lever in MI355X_MICROARCH.md's price list)
-template <bool PACKED = true, bool QUAD = false, bool LIN = false>
+// scalar VALU the SLP vectorizer cannot pair into v_pk_* (A/B builds only: SCALAR below)
+__device__ __forceinline__ float mul_s(float a, float b) {
+  float r;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float fma_s(float a, float b, float c) {
+  float r;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// SCALAR (A/B builds): the LIN / QUAD tiers in unpaired scalar fp32 (the same IEEE operations)
+template <bool PACKED = true, bool QUAD = false, bool LIN = false, bool SCALAR = false>
 __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
   float mx = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
   if (LIN && __builtin_amdgcn_ballot_w64(mx > cp.x2) == 0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = __builtin_amdgcn_exp2f(x[i] * fmaf(cp.l1, x[i] * x[i], cp.l0));
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (SCALAR) p[i] = __builtin_amdgcn_exp2f(mul_s(x[i], fma_s(cp.l1, mul_s(x[i], x[i]), cp.l0)));
+      else p[i] = __builtin_amdgcn_exp2f(x[i] * fmaf(cp.l1, x[i] * x[i], cp.l0));
+    }
   } else if (QUAD && __builtin_amdgcn_ballot_w64(mx > cp.x1) == 0) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float u = x[i] * x[i];
-      const float P = fmaf(fmaf(cp.q2, u, cp.q1), u, cp.q0);
-      p[i] = __builtin_amdgcn_exp2f(x[i] * P);
+      if constexpr (SCALAR) {
+        const float u = mul_s(x[i], x[i]);
+        p[i] = __builtin_amdgcn_exp2f(mul_s(x[i], fma_s(fma_s(cp.q2, u, cp.q1), u, cp.q0)));
+      } else {
+        const float u = x[i] * x[i];
+        const float P = fmaf(fmaf(cp.q2, u, cp.q1), u, cp.q0);
+        p[i] = __builtin_amdgcn_exp2f(x[i] * P);
+      }
     }
   } else if (__builtin_amdgcn_ballot_w64(mx > cp.x0) == 0) {
     if constexpr (PACKED) {
