@@ -169,6 +169,54 @@ def test_gemm_kernels_bitwise_equal(cuda, M, N, K, epi):
     assert bool((err <= tol).all()), float(err.max())
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 64, 256), (768, 1024, 1024), (768, 4096, 1024), (768, 1024, 4096),
+                                   (576, 768, 3072)])
+@pytest.mark.parametrize("epi", [nat.EPI_STORE, nat.EPI_GELU, 13, nat.EPI_RESID, nat.EPI_RESID_FFN,
+                                 nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16])
+def test_gemm_small_m_kernel(cuda, M, N, K, epi):
+    """gemm_bf16_small.hip (the text tower's GEMMs: 64 x 64 tiles, K split over 4 waves, partials summed
+    in LDS in wave order) against fp64 on every epilogue it takes (13 = ReLU, encoders.py:743), with
+    padded rows; the shapes are the LvT-Large / Base text tower's at 8 queries (M = 768; 576 = 9 x 64)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    w = _bf(torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.2).float().to(cuda)
+    f32_out = epi in (nat.EPI_RESID, nat.EPI_RESID_FFN)
+    resid = epi in (nat.EPI_RESID, nat.EPI_RESID_FFN, nat.EPI_RESID_BF16, nat.EPI_RESID_FFN_BF16)
+    x0 = torch.randn(M, N, generator=g).to(cuda)
+    if resid:
+        o = x0.clone() if f32_out else x0.to(torch.bfloat16)
+    else:
+        o = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    rp = None if epi == nat.EPI_STORE else pad
+    nat.dev_gemm_kernel(1, a, w, b, epi, o, resid=o if resid else None, rowpad=rp)
+    torch.cuda.synchronize()
+    y = a.double() @ w.double().T + b.double()
+    keep = (1 - pad.double())[:, None]
+    if epi == nat.EPI_STORE:
+        ref = y
+    elif epi == nat.EPI_GELU:
+        ref = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) * keep
+    elif epi == 13:
+        ref = y.clamp(min=0) * keep
+    else:
+        xr = x0.double() if f32_out else x0.to(torch.bfloat16).double()
+        ref = xr + y * keep
+    err = (o.double() - ref).abs()
+    tol = (1e-4 if f32_out else 2 ** -8 * ref.abs() + 1e-4) + 5e-6 * K ** 0.5
+    assert bool((err <= tol).all()), float(err.max())
+
+
+def test_gemm_small_m_rejects_unsupported(cuda):
+    a = torch.zeros(64, 192, dtype=torch.bfloat16, device=cuda)  # K % 256 != 0
+    w = torch.zeros(64, 192, dtype=torch.bfloat16, device=cuda)
+    b = torch.zeros(64, device=cuda)
+    o = torch.empty(64, 64, dtype=torch.bfloat16, device=cuda)
+    with pytest.raises(Exception, match="small-M GEMM"):
+        nat.dev_gemm_kernel(1, a, w, b, nat.EPI_STORE, o)
+
+
 def test_gemm_bf16_asymmetric_identity(cuda):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     M = N = K = 256

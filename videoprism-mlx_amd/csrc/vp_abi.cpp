@@ -522,7 +522,7 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
                        int64_t K, void* out, const float* bias, const void* resid, const float* pos,
                        int64_t pos_rows, const float* rowpad, void* stream) {
   using namespace vp;
-  const char* e = gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  const char* e = which == 1 ? nullptr : gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
@@ -532,8 +532,12 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
     VP_HIP(gemm_bf16_w4(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
   else if (which == 8)
     VP_HIP(gemm_bf16(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
-  else
-    return fail(VP_EINVAL, "which must be 4 or 8");
+  else if (which == 1) {  // the small-M kernel (text tower)
+    if (!gemm_bf16_small_ok(epi, (int)M, (int)N, (int)K, K, K))
+      return fail(VP_EINVAL, "small-M GEMM: epilogue 0, 1, 2, 4, 5, 7 or 13 and K % 256 == 0");
+    VP_HIP(gemm_bf16_small(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
+  } else
+    return fail(VP_EINVAL, "which must be 1, 4 or 8");
   return VP_OK;
 }
 

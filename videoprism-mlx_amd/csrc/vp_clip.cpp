@@ -75,13 +75,18 @@ ClipVideoWs clip_video_ws(const vp_clip* c, int64_t B, int64_t T, int64_t H, int
 struct ClipTextWs {
   size_t x = 0, hb = 0, big = 0, pad = 0, total = 0;
   int64_t Mt = 0;
+  bool small = false;  // bf16 GEMMs on the small-M kernel (64-row tiles)
 };
 
 ClipTextWs clip_text_ws(const vp_clip* c, int64_t Q, int64_t L) {
   const int64_t D = c->cfg.video.model_dim;
   const size_t es = c->bf16() ? 2 : 4;
   ClipTextWs w;
-  w.Mt = (Q * (L + 1) + 255) / 256 * 256;
+  // up to 4096 rows (63 queries) the bf16 GEMMs take the small-M kernel, whose tiles are 64 rows; the
+  // 256 x 256-tile kernels would leave at least three quarters of the CUs idle
+  w.small = c->bf16() && Q * (L + 1) <= 4096 && D % 256 == 0;
+  const int64_t rt = w.small ? 64 : 256;
+  w.Mt = (Q * (L + 1) + rt - 1) / rt * rt;
   size_t off = 0;
   w.x = off; off = align256(off + (size_t)w.Mt * D * 4);  // fp32 residual stream
   w.hb = off; off = align256(off + (size_t)w.Mt * D * es);
@@ -488,6 +493,7 @@ int vp_clip_encode_text(vp_clip* c, const int32_t* ids, const float* paddings, i
   f.s = s; f.bf = bf; f.M = (int)w.Mt; f.D = D; f.NH = v.num_heads; f.cap = v.atten_logit_cap;
   f.causal = c->cfg.enable_causal_atten ? 1 : 0;
   f.xs_f32 = true;
+  f.small_m = w.small;
   f.hb = ws + w.hb; f.big = ws + w.big;
   f.pf = &c->video->prof;
   f.cls_all = PC_ATTN_TEXT;  // the whole text tower in one profiler class ("text_tower"), so the vision GEMM

@@ -520,6 +520,7 @@ struct Fwd {
   float cap = 0.0f;
   int causal = 1;            // ATT_TEXT: merged causal + padding mask (enable_causal_atten)
   bool xs_f32 = false;       // bf16 GEMMs over an fp32 residual stream (text tower; no folding)
+  bool small_m = false;      // few rows (text tower): 64 x 64-tile GEMM, K split over the waves (gemm_bf16_small.hip)
   void* hb = nullptr;        // [M][D] LayerNorm / attention output
   void* big = nullptr;       // [M][max(3D, F)] q|k|v, FFN hidden
   float* st_part = nullptr;  // [D/128][M][2] partial row statistics (folded LayerNorm)
@@ -554,6 +555,8 @@ struct Fwd {
     ep.out = o; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldo;
     ep.pos = pos; ep.pos_rows = pos_rows; ep.rowpad = rowpad;
     ep.ln_rs = ln_rs; ep.ln_c = lnc; ep.st_part = st_part; ep.st_rows = M;
+    if (bf && small_m && vp::gemm_bf16_small_ok(epi, M, N, K, K, K))
+      return vp::gemm_bf16_small(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wt, K, M, N, K, ep, s);
     if (bf) return vp::gemm_bf16_auto(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wt, K, M, N, K, ep, s);
     return vp::gemm_f32(epi, (const float*)A, K, (const float*)Wt, K, M, N, K, ep, s);
   }

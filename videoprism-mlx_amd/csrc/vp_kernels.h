@@ -90,6 +90,11 @@ const char* gemm_bf16_check(int M, int N, int K, int64_t lda, int64_t ldw);
 hipError_t gemm_bf16(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                      int N, int K, const EpiArgs& ep, hipStream_t s);
 
+// small M (the text tower, gemm_bf16_small.hip): 64 x 64 tiles, K split over 4 waves; epilogues EPI_BF16,
+// EPI_GELU_BF16, EPI_RELU_BF16, EPI_RESID_F32/_FFN, EPI_RESID_BF16/_FFN_BF16; M, N % 64 == 0, K % 256 == 0
+bool gemm_bf16_small_ok(int epi, int M, int N, int K, int64_t lda, int64_t ldw);
+hipError_t gemm_bf16_small(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N, int K,
+                           const EpiArgs& ep, hipStream_t s);
 // 4-wave (one wave per SIMD, 128x128 per wave, 16x16x32 MFMA, full-line buffer_load..lds
 // staging) decomposition; needs N*ldw*2 < 4 GiB (32-bit buffer offsets); an A operand past that range
 // runs as consecutive row ranges (gemm_bf16_w4.hip)
