@@ -260,7 +260,48 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float* __r
   *reinterpret_cast<float2*>(rs_out + 2 * row) = ln_combine(pt, P);
 }
 
-// two-pass statistics straight from bf16 rows, one wave per row
+// two-pass statistics straight from bf16 rows, one wave per row.  NCH = D / 256 > 0: the row is held in
+// registers (lane: 4 values of every 256-column chunk, NCH 8-byte loads in flight), both passes from
+// there; NCH = 0: any D, element by element (each load waited for: 1.25 TB/s on the LvT-Large aux input)
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_row_stats_vec_kernel(const bf16_t* __restrict__ x, int64_t M,
+                                                               float* __restrict__ rs_out) {
+  constexpr int D = NCH * 256;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const bf16_t* r = x + row * D + 4 * lane;
+  uint2 u[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) u[j] = *reinterpret_cast<const uint2*>(r + 256 * j);
+  float v[NCH][4];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    v[j][0] = __uint_as_float(u[j].x << 16);
+    v[j][1] = __uint_as_float(u[j].x & 0xffff0000u);
+    v[j][2] = __uint_as_float(u[j].y << 16);
+    v[j][3] = __uint_as_float(u[j].y & 0xffff0000u);
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) a += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) a += __shfl_xor(a, off);
+  const float mean = a / D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[j][e] - mean;
+      q = fmaf(d, d, q);
+    }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) q += __shfl_xor(q, off);
+  const float rs = 1.0f / sqrtf(q / D + 1e-6f);
+  if (lane == 0) *reinterpret_cast<float2*>(rs_out + 2 * row) = make_float2(rs, -mean * rs);
+}
+
 __global__ __launch_bounds__(256) void ln_row_stats_kernel(const bf16_t* __restrict__ x, int64_t M, int D,
                                                            float* __restrict__ rs_out) {
   const int lane = threadIdx.x & 63;
@@ -449,7 +490,14 @@ hipError_t ln_stats_finalize(const float* st_part, int P, int64_t M, float* ln_r
 }
 
 hipError_t ln_row_stats(const bf16_t* x, int64_t M, int D, float* ln_rs, hipStream_t s) {
-  hipLaunchKernelGGL(ln_row_stats_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, x, M, D, ln_rs);
+  const dim3 g((unsigned)((M + 3) / 4));
+  switch (D) {
+    case 768: hipLaunchKernelGGL(ln_row_stats_vec_kernel<3>, g, dim3(256), 0, s, x, M, ln_rs); break;
+    case 1024: hipLaunchKernelGGL(ln_row_stats_vec_kernel<4>, g, dim3(256), 0, s, x, M, ln_rs); break;
+    case 1536: hipLaunchKernelGGL(ln_row_stats_vec_kernel<6>, g, dim3(256), 0, s, x, M, ln_rs); break;
+    case 2048: hipLaunchKernelGGL(ln_row_stats_vec_kernel<8>, g, dim3(256), 0, s, x, M, ln_rs); break;
+    default: hipLaunchKernelGGL(ln_row_stats_kernel, g, dim3(256), 0, s, x, M, D, ln_rs);
+  }
   return hipGetLastError();
 }
 

@@ -81,23 +81,27 @@ __global__ __launch_bounds__(256) void gemm_bf16_small_kernel(const bf16_t* __re
   const int klast = kend - kSmKStep;
   auto at = [&](int k) { return k < klast ? k : klast; };
   const int ns = kw / kSmKStep;
+  // one stage's 32 MFMAs with the 16 loads of the stage two ahead spread between them (one load per
+  // MFMA pair: the address unit takes a 16-row load per 2 MFMAs instead of a burst of 16)
+  auto step = [&](const Stage& sc, Stage& sl, int kl) {
+    load(sl, kl);
+    compute(sc);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+    }
+    fence();
+  };
   load(s0, kbeg);
   load(s1, at(kbeg + kSmKStep));
+  fence();
   int i = 0;
   for (; i + 3 <= ns; i += 3) {
     const int k = kbeg + i * kSmKStep;
-    load(s2, at(k + 2 * kSmKStep));
-    fence();
-    compute(s0);
-    fence();
-    load(s0, at(k + 3 * kSmKStep));
-    fence();
-    compute(s1);
-    fence();
-    load(s1, at(k + 4 * kSmKStep));
-    fence();
-    compute(s2);
-    fence();
+    step(s0, s2, at(k + 2 * kSmKStep));
+    step(s1, s0, at(k + 3 * kSmKStep));
+    step(s2, s1, at(k + 4 * kSmKStep));
   }
   if (i < ns) compute(s0);      // one or two stages left: they are in s0, s1
   if (i + 1 < ns) compute(s1);
