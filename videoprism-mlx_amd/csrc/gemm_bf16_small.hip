@@ -12,7 +12,7 @@
 // 64 x 64 fp32 partial over K/4, 16 accumulators of v_mfma_f32_16x16x32_bf16), so M = 768 gives
 // 144-768 workgroups.  Operands go global -> VGPRs in MFMA fragment order (lane: row l & 15, k-group
 // l >> 4, 16 contiguous bytes; no LDS staging: every byte is read once per workgroup), two 64-deep
-// K-steps in flight per wave beyond the one in use.  The four partials meet in LDS (64 KiB) and are summed in a fixed
+// K-steps in flight per wave.  The four partials meet in LDS (64 KiB) and are summed in a fixed
 // order, so the result does not depend on timing.  W is the MFMA A operand, so a lane's accumulator
 // holds 4 consecutive output columns of one row: the epilogue is gemm_epilogue.h's epi_store.
 #include "gemm_epilogue.h"
@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_small_kernel(const bf16_t* __re
                                                               int N, int K, EpiArgs ep) {
   __shared__ f32x4_t red[4][16][64];  // [wave][block ni*4 + mi][lane]
   const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar loop control
+  const int wv = threadIdx.x >> 6;
   const int tilesN = N / kSmT;
   const int m0 = (int)(blockIdx.x / tilesN) * kSmT;
   const int n0 = (int)(blockIdx.x % tilesN) * kSmT;
@@ -72,40 +72,19 @@ __global__ __launch_bounds__(256) void gemm_bf16_small_kernel(const bf16_t* __re
           acc[ni][mi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(st.w[h][ni], st.a[h][mi], acc[ni][mi], 0, 0, 0);
   };
 
-  // three register stages, loads two stages (1024 MFMA cycles) ahead of their use, the loop unrolled by
-  // hand over whole triples (no register copies: a copy of a stage still landing would wait for it).
-  // Every load in the loop is unconditional (past the range it re-reads the last stage, unused), so hipcc
-  // counts each wait exactly: vmcnt(32), the two younger stages stay in flight
-  Stage s0, s1, s2;
-  auto fence = [] { __builtin_amdgcn_sched_barrier(0); };
-  const int klast = kend - kSmKStep;
-  auto at = [&](int k) { return k < klast ? k : klast; };
-  const int ns = kw / kSmKStep;
-  // one stage's 32 MFMAs with the 16 loads of the stage two ahead spread between them (one load per
-  // MFMA pair: the address unit takes a 16-row load per 2 MFMAs instead of a burst of 16)
-  auto step = [&](const Stage& sc, Stage& sl, int kl) {
-    load(sl, kl);
-    compute(sc);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
-    }
-    fence();
-  };
-  load(s0, kbeg);
-  load(s1, at(kbeg + kSmKStep));
-  fence();
-  int i = 0;
-  for (; i + 3 <= ns; i += 3) {
-    const int k = kbeg + i * kSmKStep;
-    step(s0, s2, at(k + 2 * kSmKStep));
-    step(s1, s0, at(k + 3 * kSmKStep));
-    step(s2, s1, at(k + 4 * kSmKStep));
+  // two register stages, the next one's loads issued before this one's MFMAs.  (Three stages two ahead,
+  // with exact vmcnt waits -- fenced bursts or loads spread between the MFMAs -- measured 10-15 % slower
+  // in the LvT-Large forward, profiles/r05/text_tower_small_gemm.txt)
+  Stage s0, s1;
+  int k = kbeg;
+  load(s0, k);
+  for (; k + 2 * kSmKStep <= kend; k += 2 * kSmKStep) {
+    load(s1, k + kSmKStep);
+    compute(s0);
+    if (k + 2 * kSmKStep < kend) load(s0, k + 2 * kSmKStep);
+    compute(s1);
   }
-  if (i < ns) compute(s0);      // one or two stages left: they are in s0, s1
-  if (i + 1 < ns) compute(s1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the unused tail loads land before the registers are reused
+  if (k < kend) compute(s0);  // an odd number of stages: the last one is in s0
 
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni)
