@@ -38,9 +38,17 @@ __global__ __launch_bounds__(256) void gemm_bf16_small_kernel(const bf16_t* __re
   __shared__ f32x4_t red[4][16][64];  // [wave][block ni*4 + mi][lane]
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int tilesN = N / kSmT;
-  const int m0 = (int)(blockIdx.x / tilesN) * kSmT;
-  const int n0 = (int)(blockIdx.x % tilesN) * kSmT;
+  // XCD-aware tile order: workgroup b runs on XCD b % 8, and each XCD takes a contiguous range of the
+  // tiles ordered column-block-major, so an XCD's L2 holds a slice of W (about 1/8) plus A, instead of
+  // every XCD pulling all of A and W through the fabric (the grid is 8 x the largest range)
+  const int tilesM = M / kSmT;
+  const int T = tilesM * (N / kSmT);
+  const int xcd = blockIdx.x & 7;
+  const int lo = (int)(((int64_t)xcd * T) >> 3), hi = (int)(((int64_t)(xcd + 1) * T) >> 3);
+  const int t = lo + (int)(blockIdx.x >> 3);
+  if (t >= hi) return;  // whole workgroup
+  const int m0 = (t % tilesM) * kSmT;
+  const int n0 = (t / tilesM) * kSmT;
   const int r = lane & 15;
   const int kq = (lane >> 4) * 8;
   const int kw = K / 4;  // this wave's K range (K % 256 == 0: a multiple of kSmKStep)
@@ -110,7 +118,8 @@ template <int EPI>
 hipError_t launch_small(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N, int K,
                         const EpiArgs& ep, hipStream_t s) {
   VP_NOTE_KERNEL(gemm_bf16_small_kernel<EPI>);
-  const int64_t grid = (int64_t)(M / kSmT) * (N / kSmT);
+  const int64_t T = (int64_t)(M / kSmT) * (N / kSmT);
+  const int64_t grid = 8 * ((T + 7) / 8);  // 8 x the largest per-XCD range ((x + 1) T / 8 - x T / 8 <= ceil(T / 8))
   hipLaunchKernelGGL(gemm_bf16_small_kernel<EPI>, dim3((unsigned)grid), dim3(256), 0, s, A, lda, W, ldw, M, N, K, ep);
   return hipGetLastError();
 }
