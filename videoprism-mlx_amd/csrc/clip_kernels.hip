@@ -277,6 +277,19 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(const float* __restrict
     if (m0 + i < M) out[(int64_t)(m0 + i) * ldo + n] = acc[i] + red[0][i][col] + red[1][i][col] + red[2][i][col] + b;
 }
 
+// out[m][n] = bias[n] + sum_z part[z][m][n] in z order (small_gemm_splitk)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, int64_t MN,
+                                                            int N, const float* __restrict__ bias,
+                                                            float* __restrict__ out, int64_t ldo) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= MN) return;
+  float v = part[i];
+  for (int z = 1; z < splits; ++z) v += part[z * MN + i];
+  const int64_t m = i / N;
+  const int n = (int)(i % N);
+  out[m * ldo + n] = v + (bias ? bias[n] : 0.0f);
+}
+
 __global__ __launch_bounds__(256) void ln_l2_rows_kernel(const void* __restrict__ x, int in_bf16, int64_t stride,
                                                          int D, const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, int do_l2,
@@ -400,6 +413,22 @@ hipError_t small_gemm(const float* A, int64_t lda, int64_t sA, const float* Wt, 
   if (M < 1 || N < 1 || K < 1 || batch < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(small_gemm_kernel, dim3((N + kSgN - 1) / kSgN, (M + kSgM - 1) / kSgM, batch), dim3(256), 0, s, A,
                      lda, sA, Wt, sW, bias, sB, out, ldo, sO, M, N, K);
+  return hipGetLastError();
+}
+
+// K split `splits` ways as a batch of small_gemm over K slices (A columns / Wt rows), partials [splits][M][N]
+// in `part`, then summed in slice order: the same bits for any M, and splits x the workgroups of one
+// small_gemm (the pooler's output projection, K = heads x dim_per_head = 4096 on LvT-Large, otherwise ran on
+// N / 64 = 16 workgroups)
+hipError_t small_gemm_splitk(const float* A, int64_t lda, const float* Wt, const float* bias, float* out, int64_t ldo,
+                             int M, int N, int K, int splits, float* part, hipStream_t s) {
+  if (splits < 1 || K % splits) return hipErrorInvalidValue;
+  const int Kc = K / splits;
+  hipError_t e = small_gemm(A, lda, Kc, Wt, (int64_t)Kc * N, nullptr, 0, part, N, (int64_t)M * N, M, N, Kc, splits, s);
+  if (e != hipSuccess) return e;
+  const int64_t MN = (int64_t)M * N;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, part, splits, MN, N,
+                     bias, out, ldo);
   return hipGetLastError();
 }
 

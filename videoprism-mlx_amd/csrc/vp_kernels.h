@@ -185,6 +185,8 @@ int pool_chunks(int S);
 hipError_t small_gemm(const float* A, int64_t lda, int64_t sA, const float* Wt, int64_t sW, const float* bias,
                       int64_t sB, float* out, int64_t ldo, int64_t sO, int M, int N, int K, int batch,
                       hipStream_t s);
+hipError_t small_gemm_splitk(const float* A, int64_t lda, const float* Wt, const float* bias, float* out, int64_t ldo,
+                             int M, int N, int K, int splits, float* part, hipStream_t s);
 // rows r of x (stride elements apart): optional LayerNorm (gamma = 1 + scale) then optional
 // L2 normalisation, fp32 out [rows][D]
 hipError_t ln_l2_rows(const void* x, int in_bf16, int64_t stride, int rows, int D, const float* gamma,
