@@ -200,16 +200,18 @@ int run_pooler(Fwd& f, const PoolerW& pw, const void* feat, int M, int G, int Sg
     hipError_t e = pool_logits(feat, f.bf, M, Sg, D, pw.U, (const bf16_t*)pw.Ut, NH, sc.logits, f.s);
     if (e != hipSuccess) return e;
     return pool_softmax_wsum(feat, f.bf, G, Sg, D, NH, sc.logits, sc.stats, sc.zpart, sc.z, f.s); }));
-  VP_HIP(small_gemm(sc.z, (int64_t)NH * D, D, pw.WvT, (int64_t)D * dp, pw.bv, dp, sc.enc, (int64_t)NH * dp, dp, G,
-                    dp, D, NH, f.s));
-  // output projection over K = NH * dp, split 8 ways into zpart (free again: z is summed; it holds
-  // >= G * NH * D floats, splits <= NH)
+  // the value projection per head, then the output projection over K = NH * dp split 8 ways into zpart (free
+  // again: z is summed; it holds >= G * NH * D floats, splits <= NH), then LayerNorm (+ L2)
   const int splits = NH >= 8 && (NH * dp) % (8 * 128) == 0 ? 8 : 1;
-  if (splits > 1)
-    VP_HIP(small_gemm_splitk(sc.enc, (int64_t)NH * dp, pw.WpT, pw.bp, sc.pooled, D, G, D, NH * dp, splits, sc.zpart, f.s));
-  else
-    VP_HIP(small_gemm(sc.enc, (int64_t)NH * dp, 0, pw.WpT, 0, pw.bp, 0, sc.pooled, D, 0, G, D, NH * dp, 1, f.s));
-  VP_HIP(ln_l2_rows(sc.pooled, 0, D, G, D, pw.ln_g, pw.ln_b, do_l2, dst, f.s));
+  VP_HIP(f.rec(PC_POOL, 2.0 * G * D * (double)dp * NH * 2.0, 4.0 * (double)NH * D * dp * 2.0, [&] {
+    hipError_t e = small_gemm(sc.z, (int64_t)NH * D, D, pw.WvT, (int64_t)D * dp, pw.bv, dp, sc.enc, (int64_t)NH * dp,
+                              dp, G, dp, D, NH, f.s);
+    if (e != hipSuccess) return e;
+    e = splits > 1 ? small_gemm_splitk(sc.enc, (int64_t)NH * dp, pw.WpT, pw.bp, sc.pooled, D, G, D, NH * dp, splits,
+                                       sc.zpart, f.s)
+                   : small_gemm(sc.enc, (int64_t)NH * dp, 0, pw.WpT, 0, pw.bp, 0, sc.pooled, D, 0, G, D, NH * dp, 1, f.s);
+    if (e != hipSuccess) return e;
+    return ln_l2_rows(sc.pooled, 0, D, G, D, pw.ln_g, pw.ln_b, do_l2, dst, f.s); }));
   return VP_OK;
 }
 
