@@ -193,8 +193,34 @@ def g12_lvt_base_t40():
     np.savez_compressed(os.path.join(HERE, "g12_lvt_base_t40.npz"), **arrays)
 
 
+# g13: full-depth LvT-Base video embeddings of 8 clips (the construction of
+# tests/test_gpu_clip.py::test_clip_full_lvt_base_bf16 at seeds 11..18: synthetic parameters and frames of the
+# seed, B = 1, T = 8) in fp64, and the cast floor of each (fp64 arithmetic on bf16-rounded parameters and frames,
+# mode 'wbf16'): the multi-clip bf16 gate of test_clip_lvt_base_bf16_over_clips.  ~40 s of oracle per clip.
+G13_SEEDS = list(range(11, 19))
+
+
+def bf16_round(a):
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32).view(np.float32)
+
+
+def g13_lvt_base_clips():
+    cfg = dict(models.CONFIGS["videoprism_lvt_v1_base"])
+    cfg["vocabulary_size"] = 1000
+    f64, cast = [], []
+    for seed in G13_SEEDS:
+        var = params.synthetic_params(cfg, seed, specs=params.clip_leaf_specs(cfg))
+        x = np.random.default_rng(seed).random((1, 8, 288, 288, 3), dtype=np.float32)
+        f64.append(orc.video_clip(var["params"], cfg, x, None, None, "f64")[0][0])
+        cast.append(orc.video_clip(var["params"], cfg, bf16_round(x), None, None, "wbf16")[0][0])
+    np.savez_compressed(os.path.join(HERE, "g13_lvt_base_clips.npz"), seeds=np.array(G13_SEEDS),
+                        vocabulary_size=np.array(1000), T=np.array(8), video_emb_f64=np.stack(f64),
+                        cast_floor_emb=np.stack(cast))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12"]
+    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13"]
     if "g1" in which:
         g1_tiny()
     if "g2" in which:
@@ -213,6 +239,8 @@ if __name__ == "__main__":
         g8_lvt_large_t16()
     if "g12" in which:
         g12_lvt_base_t40()
+    if "g13" in which:
+        g13_lvt_base_clips()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -218,3 +218,15 @@ def test_dot_atten_query_blocks_equal_whole(monkeypatch, mode):
         blocked = orc.dot_atten(q, k, v, mask, nm, 50.0, H)
         monkeypatch.undo()
         np.testing.assert_allclose(blocked, whole, rtol=0, atol=1e-14 if mode == "f64" else 0)
+
+
+def test_golden_lvt_base_clips_fixture():
+    """g13 (the multi-clip LvT-Base bf16 gate): L2-normalised fp64 embeddings of 8 clips, and cast floors
+    that are the bf16 noise the gate measures against -- non-zero and of the order of the 1e-3 bar."""
+    g = np.load(os.path.join(GOLD, "g13_lvt_base_clips.npz"))
+    assert list(g["seeds"]) == list(range(11, 19))
+    e, c = g["video_emb_f64"], g["cast_floor_emb"]
+    assert e.shape == c.shape == (8, 768)
+    np.testing.assert_allclose(np.linalg.norm(e, axis=-1), 1.0, rtol=1e-12)
+    floor = np.abs(c - e).max(axis=-1)
+    assert bool(((floor > 5e-4) & (floor < 2e-3)).all()), floor
