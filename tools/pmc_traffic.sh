@@ -3,11 +3,11 @@
 # group (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass), then the per-symbol
 # traffic record bench.py reads for roofline.traffic.
 # Usage (on the GPU box, from the repo root): tools/pmc_traffic.sh OUTDIR WORKLOAD [RECORD]
-#   RECORD defaults to profiles/traffic_r04_WORKLOAD.json
+#   RECORD defaults to profiles/traffic_r05_WORKLOAD.json
 set -e
 OUT=$(realpath -m "$1")
 WL=${2:-base}
-REC=${3:-profiles/traffic_r04_${WL}.json}
+REC=${3:-profiles/traffic_r05_${WL}.json}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
