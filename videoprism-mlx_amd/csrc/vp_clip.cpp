@@ -189,6 +189,7 @@ int pack_pooler(Hd* c, const std::string& root, int64_t D, int64_t H, int64_t dp
 // pooler over G groups of Sg rows of feat [G*Sg][D] -> dst [G][D] fp32 (LayerNorm, then L2 if do_l2)
 struct PoolScratch {
   float *logits, *stats, *zpart, *z, *enc, *pooled;
+  size_t zpart_floats;  // capacity of zpart (the output projection's split-K partials reuse it)
 };
 
 int run_pooler(Fwd& f, const PoolerW& pw, const void* feat, int M, int G, int Sg, int D, int NH,
@@ -201,8 +202,8 @@ int run_pooler(Fwd& f, const PoolerW& pw, const void* feat, int M, int G, int Sg
     if (e != hipSuccess) return e;
     return pool_softmax_wsum(feat, f.bf, G, Sg, D, NH, sc.logits, sc.stats, sc.zpart, sc.z, f.s); }));
   // the value projection per head, then the output projection over K = NH * dp split 8 ways into zpart (free
-  // again: z is summed; it holds >= G * NH * D floats, splits <= NH), then LayerNorm (+ L2)
-  const int splits = NH >= 8 && (NH * dp) % (8 * 128) == 0 ? 8 : 1;
+  // again once z is summed; sized for >= G * NH * D floats), then LayerNorm (+ L2)
+  const int splits = NH >= 8 && (NH * dp) % (8 * 128) == 0 && (size_t)8 * G * D <= sc.zpart_floats ? 8 : 1;
   VP_HIP(f.rec(PC_POOL, 2.0 * G * D * (double)dp * NH * 2.0, 4.0 * (double)NH * D * dp * 2.0, [&] {
     hipError_t e = small_gemm(sc.z, (int64_t)NH * D, D, pw.WvT, (int64_t)D * dp, pw.bv, dp, sc.enc, (int64_t)NH * dp,
                               dp, G, dp, D, NH, f.s);
@@ -417,7 +418,7 @@ int clip_video_chunk(vp_clip* c, const void* video, int in_dtype, int64_t B, int
   float* z = reinterpret_cast<float*>(ws + L.z);
   float* enc = reinterpret_cast<float*>(ws + L.enc);
   float* pooled = reinterpret_cast<float*>(ws + L.pooled);
-  const PoolScratch sc{logits, stats, zpart, z, enc, pooled};
+  const PoolScratch sc{logits, stats, zpart, z, enc, pooled, (L.z - L.zpart) / 4};
   auto pool = [&](int G, int Sg, float* dst) -> int {
     return run_pooler(f, c->pool, feat, M, G, Sg, D, NH, sc, normalize, dst);
   };
@@ -681,7 +682,8 @@ int classifier_chunk(vp_classifier* c, const void* video, int in_dtype, int64_t 
   float* emb = embeddings ? embeddings : reinterpret_cast<float*>(ws + L.total);
   const PoolScratch sc{reinterpret_cast<float*>(ws + L.logits), reinterpret_cast<float*>(ws + L.stats),
                        reinterpret_cast<float*>(ws + L.zpart), reinterpret_cast<float*>(ws + L.z),
-                       reinterpret_cast<float*>(ws + L.enc), reinterpret_cast<float*>(ws + L.pooled)};
+                       reinterpret_cast<float*>(ws + L.enc), reinterpret_cast<float*>(ws + L.pooled),
+                       (L.z - L.zpart) / 4};
   if ((rc = run_pooler(f, c->pool, feat, M, (int)B, (int)(T * N), D, NH, sc, 0, emb))) return rc;
   VP_HIP(small_gemm(emb, D, 0, c->wproj, 0, c->bproj, 0, logits, c->num_classes, 0, (int)B, c->num_classes, D, 1, s));
   return VP_OK;
