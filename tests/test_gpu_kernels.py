@@ -280,7 +280,10 @@ def _oracle_attention(qkv, num_seq, S, heads, cap, key_pad=None):
 # scale 0.125 keeps the logits in the one-transcendental polynomial range (vp_common.h
 # capped_exp16); the larger scales exercise the exact path
 @pytest.mark.parametrize("S,num_seq,heads,scale", [(256, 3, 12, 1.0), (256, 2, 16, 4.0), (256, 2, 12, 0.125),
-                                                   (16, 40, 12, 1.0), (8, 9, 12, 3.0), (5, 7, 16, 1.0)])
+                                                   (16, 40, 12, 1.0), (8, 9, 12, 3.0), (5, 7, 16, 1.0),
+                                                   (17, 9, 12, 1.0), (32, 10, 12, 3.0), (40, 5, 16, 1.0),
+                                                   (64, 9, 12, 1.0), (100, 3, 12, 4.0), (128, 5, 16, 1.0),
+                                                   (200, 3, 12, 1.0)])
 def test_attention_bf16(cuda, S, num_seq, heads, scale):
     qkv = _bf(_qkv(num_seq, S, heads, S + num_seq, scale)).to(cuda)
     out = nat.op_attention(qkv, num_seq, S, heads, 50.0)
@@ -315,7 +318,7 @@ def test_attention_bf16_saturated_logits_large_v(cuda, S, num_seq, heads, cap):
     assert np.all(err <= 2 ** -8 * (np.abs(ref) + vmax)), err.max()
 
 
-@pytest.mark.parametrize("S,num_seq", [(256, 3), (16, 10), (8, 6)])
+@pytest.mark.parametrize("S,num_seq", [(256, 3), (16, 10), (8, 6), (40, 11), (64, 9), (130, 3)])
 def test_attention_bf16_key_padding(cuda, S, num_seq):
     heads = 12
     qkv = _bf(_qkv(num_seq, S, heads, 3)).to(cuda)

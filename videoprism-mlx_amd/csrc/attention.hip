@@ -262,6 +262,142 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
 }
 
 // ------------------------------------------------------------------------------------
+// sequences of 16 < S <= 256 (temporal attention of clips longer than 16 frames): the spatial
+// kernel's tiles over 256 query / key slots per workgroup, holding 256 / Sp sequences of one head,
+// Sp = S rounded up to 32, 64, 128 or 256.  Wave w's 32 queries lie in one sequence and run over that
+// sequence's Sp / 32 key tiles; slots past S are masked keys and unstored queries.  K and V are
+// staged whole (LDS-DMA, then one barrier: no chunk pipelining), the numerators are the spatial
+// kernel's exact capped form, P is rounded to bf16 for O^T = V^T.P^T and the row sum is fp32.
+// ------------------------------------------------------------------------------------
+constexpr int kSqLds = 2 * kSpS * 128 + kSpS * 4 + 8 * 4;  // K, V, key paddings, 8 all-masked flags
+
+template <bool MASK>
+__global__ __launch_bounds__(kSpThreads, 4) void attn_seq_kernel(const bf16_t* __restrict__ qkv,
+                                                                bf16_t* __restrict__ o, int num_seq, int S,
+                                                                int Sp, int heads, float cap,
+                                                                const float* __restrict__ key_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Ks = smem;
+  char* Vs = smem + kSpS * 128;
+  float* kp = reinterpret_cast<float*>(smem + 2 * kSpS * 128);  // [slot] key padding (MASK)
+  int* allmask = reinterpret_cast<int*>(kp + kSpS);              // [sequence of the workgroup]
+  const int D = heads * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const int per = kSpS / Sp;  // sequences per workgroup
+  const int h = (int)blockIdx.x % heads;
+  const int seq0 = (int)blockIdx.x / heads * per;
+  const int lane = threadIdx.x & 63;
+  const int w = wave_id();
+  // slot -> q|k|v row of this head (slots past S or past the last sequence read a valid row, unused)
+  auto row_of = [&](int slot) {
+    const int j = slot / Sp, t = slot - j * Sp;
+    const int sq = seq0 + j < num_seq ? seq0 + j : num_seq - 1;
+    return (int64_t)sq * S + (t < S ? t : S - 1);
+  };
+  // K and V: 64 pieces of 8 slots x 128 B, 8 per wave; the bank swizzle goes on the source address
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int piece = i * 8 + w;
+    const int isV = piece >> 5;
+    const int slot = (piece & 31) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (isV ? swzV(slot) : swzK(slot));
+    const bf16_t* src = qkv + row_of(slot) * ld + (isV ? 2 * D : D) + h * 64 + c * 8;
+    __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(smem + piece * 1024), 16, 0, 0);
+  }
+  const int q0 = w * 32;
+  const int half = lane >> 5;
+  const int j = q0 / Sp;  // this wave's sequence in the workgroup
+  bf16x8 qf[4];
+  {
+    const bf16_t* qp = qkv + row_of(q0 + (lane & 31)) * ld + h * 64 + 8 * half;
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) qf[kd] = *reinterpret_cast<const bf16x8*>(qp + 16 * kd);
+  }
+  if constexpr (MASK) {
+    if (threadIdx.x < kSpS) {
+      const int jj = threadIdx.x / Sp, t = threadIdx.x - jj * Sp;
+      kp[threadIdx.x] = (t < S && seq0 + jj < num_seq) ? key_pad[(int64_t)(seq0 + jj) * S + t] : 1.0f;
+    }
+    if (threadIdx.x < 8) allmask[threadIdx.x] = 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (MASK) {
+    if (threadIdx.x < kSpS && (threadIdx.x % Sp) < S && kp[threadIdx.x] == 0.0f) allmask[threadIdx.x / Sp] = 0;
+    __syncthreads();
+  }
+  const bool all_masked = MASK && allmask[j] != 0;
+
+  const float c1 = 2.0f * kLog2e / cap;
+  const float c2 = cap * kLog2e;
+  f32x16 y0 = {}, y1 = {};
+  float lsum = 0.0f;
+  const int krow_l = lane & 31;
+  const int g = lane >> 4;
+  const int li = lane & 15;
+  const int trq = li >> 2, trp = li & 3;
+  const int kt0 = j * Sp / 32, kt1 = kt0 + Sp / 32;
+#pragma unroll 1
+  for (int kt = kt0; kt < kt1; ++kt) {
+    f32x16 x = {};
+    const int krow = kt * 32 + krow_l;
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) {
+      const int c = 2 * kd + half;
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + krow * 128 + ((c ^ swzK(krow)) << 4));
+      x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kd], x, 0, 0, 0);
+    }
+    // register i <-> key slot kt*32 + (i&3) + 8(i>>2) + 4*half
+    float p[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int slot = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
+      float e = capped_exp(x[i], c1, c2);
+      if constexpr (MASK) e = all_masked ? 1.0f : (kp[slot] != 0.0f ? 0.0f : e);
+      if (slot - j * Sp >= S) e = 0.0f;
+      p[i] = e;
+      lsum += e;
+    }
+    bf16x8 pf[2];
+#pragma unroll
+    for (int sidx = 0; sidx < 2; ++sidx) {
+      uint32_t u[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) u[jj] = pack_bf16x2(p[8 * sidx + 2 * jj], p[8 * sidx + 2 * jj + 1]);
+      pf[sidx] = *reinterpret_cast<bf16x8*>(u);
+    }
+#pragma unroll
+    for (int sidx = 0; sidx < 2; ++sidx) {
+      const int key = kt * 32 + 16 * sidx + 4 * half + trq;
+#pragma unroll
+      for (int dh = 0; dh < 2; ++dh) {
+        const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
+        const int c = col >> 3;
+        const char* a = Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2;
+        const bf16x4 lo = tr_read(a), hi = tr_read(a + 8 * 128);
+        const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dh == 0) y0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[sidx], y0, 0, 0, 0);
+        else y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[sidx], y1, 0, 0, 0);
+      }
+    }
+  }
+  lsum += __shfl_xor(lsum, 32);
+  const float inv = 1.0f / lsum;
+  const int slot = q0 + (lane & 31);
+  const int t = slot - j * Sp;
+  if (t >= S || seq0 + j >= num_seq) return;
+  // y_dh[i] = O^T[d = 32dh + (i&3) + 8(i>>2) + 4*half][query]: 4 consecutive dims per register quad
+  bf16_t* op = o + ((int64_t)(seq0 + j) * S + t) * D + h * 64 + 4 * half;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    *reinterpret_cast<uint2*>(op + 8 * g4) = make_uint2(pack_bf16x2(y0[4 * g4] * inv, y0[4 * g4 + 1] * inv),
+                                                        pack_bf16x2(y0[4 * g4 + 2] * inv, y0[4 * g4 + 3] * inv));
+    *reinterpret_cast<uint2*>(op + 32 + 8 * g4) = make_uint2(pack_bf16x2(y1[4 * g4] * inv, y1[4 * g4 + 1] * inv),
+                                                             pack_bf16x2(y1[4 * g4 + 2] * inv, y1[4 * g4 + 3] * inv));
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // temporal: S <= 16, dh = 64; one wave per (sequence, head)
 // ------------------------------------------------------------------------------------
 constexpr int kTpWaves = 4;
@@ -478,6 +614,30 @@ hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, in
     hipLaunchKernelGGL(attn_temporal_kernel<true>, grid, dim3(kTpWaves * 64), 0, s, qkv, o, pairs, S, heads, cap, key_pad);
   else
     hipLaunchKernelGGL(attn_temporal_kernel<false>, grid, dim3(kTpWaves * 64), 0, s, qkv, o, pairs, S, heads, cap, key_pad);
+  return hipGetLastError();
+}
+
+hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap,
+                              const float* key_pad, hipStream_t s) {
+  if (!(cap > 0.0f) || S < 17 || S > kSpS || num_seq < 1) return hipErrorInvalidValue;
+  const int Sp = S <= 32 ? 32 : S <= 64 ? 64 : S <= 128 ? 128 : 256;
+  const int per = kSpS / Sp;
+  const void* fn = key_pad ? (const void*)attn_seq_kernel<true> : (const void*)attn_seq_kernel<false>;
+  static bool attr[2] = {false, false};
+  if (!attr[key_pad ? 1 : 0]) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSqLds);
+    if (e != hipSuccess) return e;
+    attr[key_pad ? 1 : 0] = true;
+  }
+  const int64_t grid = (int64_t)((num_seq + per - 1) / per) * heads;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  VP_NOTE_KERNEL(fn);
+  if (key_pad)
+    hipLaunchKernelGGL(attn_seq_kernel<true>, dim3((unsigned)grid), dim3(kSpThreads), kSqLds, s, qkv, o, num_seq, S,
+                       Sp, heads, cap, key_pad);
+  else
+    hipLaunchKernelGGL(attn_seq_kernel<false>, dim3((unsigned)grid), dim3(kSpThreads), kSqLds, s, qkv, o, num_seq, S,
+                       Sp, heads, cap, key_pad);
   return hipGetLastError();
 }
 

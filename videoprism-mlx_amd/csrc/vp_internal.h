@@ -631,13 +631,15 @@ struct Fwd {
           if (bf) return attention_long_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, s);
           return attention_masked(big, hb, 0, num_seq, S, NH, cap, nullptr, 0, s);
         }
-        // other patch grids (S != 256) and T > 16 use the generic fp32-math kernel
+        // 16 < S <= 256 (T > 16 frames, other patch grids) on the sequence-packed MFMA kernel; longer sequences
+        // on the generic fp32-math kernel
         if (!bf) {
           if (S <= 256) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, cap, pad, s);
           return attention_masked(big, hb, 0, num_seq, S, NH, cap, pad, 0, s);
         }
         if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, cap, pad, s, sblk);
         if (S <= 16) return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s);
+        if (S <= 256) return attention_seq_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s);
         return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s); }));
       VP_HIP(rec(PC_GEMM_POST, 2.0 * dM * dD * dD, gbytes(dD, dD, dE, dE), [&] {
         return gemm(fold ? EPI_RESID_BF16_ST : epi_resid, hb, D, lw.wpost, D, xs, D, lw.bpost, xs, nullptr, 1,
