@@ -58,8 +58,11 @@ def test_attention_long_bf16(cuda, S, num_seq, heads, scale):
 
 
 @pytest.mark.parametrize("bf16", [False, True])
-@pytest.mark.parametrize("S,num_seq,causal", [(65, 4, True), (65, 3, False), (130, 2, True), (7, 5, True)])
+@pytest.mark.parametrize("S,num_seq,causal", [(65, 4, True), (65, 3, False), (130, 2, True), (7, 5, True),
+                                             (33, 9, True), (256, 2, True), (300, 2, True)])
 def test_attention_masked(cuda, bf16, S, num_seq, causal):
+    """Causal + key-padding merge (layers.py:111-179): bf16 16 < S <= 256 runs on the MFMA sequence kernel (the
+    text tower's path), S <= 16, S > 256 and fp32 on the generic kernel."""
     heads = 12
     qkv = _qkv(num_seq, S, heads, S * 7 + num_seq)
     if bf16:

@@ -275,7 +275,7 @@ template <bool MASK>
 __global__ __launch_bounds__(kSpThreads, 4) void attn_seq_kernel(const bf16_t* __restrict__ qkv,
                                                                 bf16_t* __restrict__ o, int num_seq, int S,
                                                                 int Sp, int heads, float cap,
-                                                                const float* __restrict__ key_pad) {
+                                                                const float* __restrict__ key_pad, int causal) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Ks = smem;
   char* Vs = smem + kSpS * 128;
@@ -326,7 +326,11 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_seq_kernel(const bf16_t* _
     if (threadIdx.x < kSpS && (threadIdx.x % Sp) < S && kp[threadIdx.x] == 0.0f) allmask[threadIdx.x / Sp] = 0;
     __syncthreads();
   }
-  const bool all_masked = MASK && allmask[j] != 0;
+  // causal (text tower, layers.py:111-179 merged with the key paddings): key t <= query t; a padded query's row is
+  // fully masked, so its weights are uniform over all S keys (as attention_masked and the reference's softmax of
+  // equal logits); otherwise a sequence with every key padded gets uniform weights
+  const int qt = q0 + (lane & 31) - j * Sp;
+  const bool all_masked = MASK && (causal ? kp[q0 + (lane & 31)] != 0.0f : allmask[j] != 0);
 
   const float c1 = 2.0f * kLog2e / cap;
   const float c2 = cap * kLog2e;
@@ -353,6 +357,7 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_seq_kernel(const bf16_t* _
     for (int i = 0; i < 16; ++i) {
       const int slot = kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
       float e = capped_exp(x[i], c1, c2);
+      if (causal && slot - j * Sp > qt) e = 0.0f;
       if constexpr (MASK) e = all_masked ? 1.0f : (kp[slot] != 0.0f ? 0.0f : e);
       if (slot - j * Sp >= S) e = 0.0f;
       p[i] = e;
@@ -618,7 +623,7 @@ hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, in
 }
 
 hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap,
-                              const float* key_pad, hipStream_t s) {
+                              const float* key_pad, hipStream_t s, int causal) {
   if (!(cap > 0.0f) || S < 17 || S > kSpS || num_seq < 1) return hipErrorInvalidValue;
   const int Sp = S <= 32 ? 32 : S <= 64 ? 64 : S <= 128 ? 128 : 256;
   const int per = kSpS / Sp;
@@ -634,10 +639,10 @@ hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, 
   VP_NOTE_KERNEL(fn);
   if (key_pad)
     hipLaunchKernelGGL(attn_seq_kernel<true>, dim3((unsigned)grid), dim3(kSpThreads), kSqLds, s, qkv, o, num_seq, S,
-                       Sp, heads, cap, key_pad);
+                       Sp, heads, cap, key_pad, causal);
   else
     hipLaunchKernelGGL(attn_seq_kernel<false>, dim3((unsigned)grid), dim3(kSpThreads), kSqLds, s, qkv, o, num_seq, S,
-                       Sp, heads, cap, key_pad);
+                       Sp, heads, cap, key_pad, causal);
   return hipGetLastError();
 }
 

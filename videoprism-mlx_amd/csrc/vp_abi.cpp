@@ -655,8 +655,13 @@ int vp_op_attention_masked(int precision, const void* qkv, void* o, int64_t num_
   using namespace vp;
   if (!qkv || !o || num_seq < 1 || heads < 1 || S < 1) return fail(VP_EINVAL, "bad argument");
   if (precision != VP_F32 && precision != VP_BF16) return fail(VP_EINVAL, "bad precision");
-  VP_HIP(attention_masked(qkv, o, precision == VP_BF16, (int)num_seq, (int)S, (int)heads, cap, key_pad, causal,
-                          static_cast<hipStream_t>(stream)));
+  // the forward's choice (vp_internal.h run_stack, ATT_TEXT): bf16 16 < S <= 256 on the MFMA sequence kernel
+  if (precision == VP_BF16 && fast_cap(cap) && S > 16 && S <= 256)
+    VP_HIP(attention_seq_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, key_pad,
+                              static_cast<hipStream_t>(stream), causal ? 1 : 0));
+  else
+    VP_HIP(attention_masked(qkv, o, precision == VP_BF16, (int)num_seq, (int)S, (int)heads, cap, key_pad, causal,
+                            static_cast<hipStream_t>(stream)));
   return VP_OK;
 }
 

@@ -623,7 +623,11 @@ struct Fwd {
           return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
       }
       if (!tattn) VP_HIP(rec(acls, aflops, abytes, [&] {
-        if (kind == ATT_TEXT) return attention_masked(big, hb, bf, num_seq, S, NH, cap, pad, causal, s);
+        if (kind == ATT_TEXT) {
+          if (bf && fast_cap(cap) && S > 16 && S <= 256)
+            return attention_seq_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s, causal);
+          return attention_masked(big, hb, bf, num_seq, S, NH, cap, pad, causal, s);
+        }
         // the bf16 kernels' max-free softmax needs 0 < cap <= kMaxFastCap; cap <= 0 (no capping,
         // layers.py:586-589) or a larger cap runs the online-softmax kernel
         if (bf && !fast_cap(cap)) return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s);

@@ -132,9 +132,10 @@ hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_
 // blk: qkv in the row-blocked layout of EPI_BF16_LN_BLK ([M/16][3D/32][16][32])
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads,
                                   float cap, const float* key_pad, hipStream_t s, bool blk = false);
-// 16 < S <= 256 (temporal attention of clips longer than 16 frames), key paddings optional (attention.hip)
+// 16 < S <= 256 (temporal attention of clips longer than 16 frames, other patch grids, the text tower with
+// causal = 1), key paddings optional (attention.hip)
 hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap,
-                              const float* key_pad, hipStream_t s);
+                              const float* key_pad, hipStream_t s, int causal = 0);
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s);
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
