@@ -148,8 +148,9 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
 
 /* Capped attention over rows qkv[num_seq*S, 3*heads*64] = [q|k|v] (q pre-scaled), writing
  * o[num_seq*S, heads*64].  Replaces DotProductAttention._dot_atten (layers.py:601-661).
- * precision VP_BF16 (S == 256 or S <= 16; S a multiple of 256 without key_pad: the long-sequence
- * kernel of the LvT auxiliary encoder) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL.
+ * precision VP_BF16 (S <= 256: the spatial kernel at S == 256, the temporal kernel at S <= 16,
+ * the sequence-packed kernel between; S a multiple of 256 without key_pad: the long-sequence kernel of
+ * the LvT auxiliary encoder) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL.
  * bf16 with a cap outside (0, 50] (no capping, or one whose unnormalised fp32 numerators could
  * overflow) runs the online-softmax kernel of vp_op_attention_masked, any S. */
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
@@ -172,10 +173,12 @@ int vp_op_patchify(const void* video, int in_dtype, void* patches, int out_dtype
 int vp_op_pool_l2(const void* emb, int dtype, int64_t B, int64_t L, int64_t D, float* out,
                   void* stream);
 
-/* Generic fp32-math attention over rows qkv[num_seq*S, 3*heads*64] (q pre-scaled), any S, with
- * key paddings key_pad [num_seq*S] (nullable) and, if causal, the merged causal + padding mask of
+/* Attention over rows qkv[num_seq*S, 3*heads*64] (q pre-scaled), any S, with key paddings
+ * key_pad [num_seq*S] (nullable) and, if causal, the merged causal + padding mask of
  * layers.py:111-179 (a padded query row is fully masked -> uniform weights).  qkv / o in
- * `precision` (VP_F32 or VP_BF16).  cap <= 0 disables the tanh cap.  Used by the text tower. */
+ * `precision` (VP_F32 or VP_BF16).  cap <= 0 disables the tanh cap.  Used by the text tower: bf16
+ * with 16 < S <= 256 and 0 < cap <= 50 on the sequence-packed MFMA kernel, otherwise fp32 math with an
+ * online softmax. */
 int vp_op_attention_masked(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,
                            int64_t heads, float cap, const float* key_pad, int causal, void* stream);
 
