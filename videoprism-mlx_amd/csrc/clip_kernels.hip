@@ -149,9 +149,10 @@ constexpr int kPwRows = 256;  // rows per chunk
 constexpr int kPwMaxH = 16;
 
 // zpart[g][c][h][d] = sum over rows of chunk c of p[g,h,s] x[g*S+s][d]: a workgroup owns one
-// (g, 256-row chunk, 256-column quarter); a thread owns one column and all 16 head sums, the
-// probabilities of the chunk sit in LDS (float4 broadcast reads)
-__global__ __launch_bounds__(256) void pool_wsum_kernel(const void* __restrict__ x, int in_bf16, int S, int D,
+// (g, 256-row chunk, 256-column quarter) with 128 threads; a thread owns two adjacent columns (one 4-byte
+// bf16 pair / 8-byte fp32 pair per row) and all 16 head sums of each, the probabilities of the chunk sit in
+// LDS (float4 broadcast reads).  Each column is summed over the rows in row order.
+__global__ __launch_bounds__(128) void pool_wsum_kernel(const void* __restrict__ x, int in_bf16, int S, int D,
                                                         int H, const float* __restrict__ logits,
                                                         const float* __restrict__ stats, int C,
                                                         float* __restrict__ zpart) {
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256) void pool_wsum_kernel(const void* __restrict__
   const int c = gc % C;
   const int r0 = c * kPwRows;
   const int nr = S - r0 < kPwRows ? S - r0 : kPwRows;
-  for (int i = threadIdx.x; i < kPwRows * kPwMaxH; i += 256) {
+  for (int i = threadIdx.x; i < kPwRows * kPwMaxH; i += 128) {
     const int r = i / kPwMaxH, h = i % kPwMaxH;
     float p = 0.0f;
     if (r < nr && h < H) {
@@ -173,35 +174,47 @@ __global__ __launch_bounds__(256) void pool_wsum_kernel(const void* __restrict__
     ps[r][h] = p;
   }
   __syncthreads();
-  const int d = q * 256 + threadIdx.x;
-  float acc[kPwMaxH];
+  const int d = q * 256 + 2 * threadIdx.x;
+  float acc0[kPwMaxH], acc1[kPwMaxH];
 #pragma unroll
-  for (int h = 0; h < kPwMaxH; ++h) acc[h] = 0.0f;
+  for (int h = 0; h < kPwMaxH; ++h) acc0[h] = acc1[h] = 0.0f;
   const int64_t rowbase = (int64_t)g * S + r0;
-  auto row = [&](int r, float xv) {
+  auto ld2 = [&](int r) -> float2 {
+    const int64_t i = (rowbase + r) * D + d;
+    if (in_bf16) {
+      const uint32_t u = *reinterpret_cast<const uint32_t*>(static_cast<const bf16_t*>(x) + i);
+      return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+    }
+    return *reinterpret_cast<const float2*>(static_cast<const float*>(x) + i);
+  };
+  auto row = [&](int r, float2 xv) {
     const float4* pr = reinterpret_cast<const float4*>(ps[r]);
 #pragma unroll
     for (int h4 = 0; h4 < kPwMaxH / 4; ++h4) {
       const float4 p = pr[h4];
-      acc[4 * h4] = fmaf(p.x, xv, acc[4 * h4]);
-      acc[4 * h4 + 1] = fmaf(p.y, xv, acc[4 * h4 + 1]);
-      acc[4 * h4 + 2] = fmaf(p.z, xv, acc[4 * h4 + 2]);
-      acc[4 * h4 + 3] = fmaf(p.w, xv, acc[4 * h4 + 3]);
+      acc0[4 * h4] = fmaf(p.x, xv.x, acc0[4 * h4]);
+      acc0[4 * h4 + 1] = fmaf(p.y, xv.x, acc0[4 * h4 + 1]);
+      acc0[4 * h4 + 2] = fmaf(p.z, xv.x, acc0[4 * h4 + 2]);
+      acc0[4 * h4 + 3] = fmaf(p.w, xv.x, acc0[4 * h4 + 3]);
+      acc1[4 * h4] = fmaf(p.x, xv.y, acc1[4 * h4]);
+      acc1[4 * h4 + 1] = fmaf(p.y, xv.y, acc1[4 * h4 + 1]);
+      acc1[4 * h4 + 2] = fmaf(p.z, xv.y, acc1[4 * h4 + 2]);
+      acc1[4 * h4 + 3] = fmaf(p.w, xv.y, acc1[4 * h4 + 3]);
     }
   };
   int r = 0;
-  for (; r + 8 <= nr; r += 8) {
-    float xv[8];
+  for (; r + 16 <= nr; r += 16) {
+    float2 xv[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xv[u] = ldx(x, in_bf16, (rowbase + r + u) * D + d);
+    for (int u = 0; u < 16; ++u) xv[u] = ld2(r + u);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) row(r + u, xv[u]);
+    for (int u = 0; u < 16; ++u) row(r + u, xv[u]);
   }
-  for (; r < nr; ++r) row(r, ldx(x, in_bf16, (rowbase + r) * D + d));
+  for (; r < nr; ++r) row(r, ld2(r));
   float* zp = zpart + ((int64_t)g * C + c) * H * D + d;
 #pragma unroll
   for (int h = 0; h < kPwMaxH; ++h)
-    if (h < H) zp[(int64_t)h * D] = acc[h];
+    if (h < H) *reinterpret_cast<float2*>(zp + (int64_t)h * D) = make_float2(acc0[h], acc1[h]);
 }
 
 __global__ __launch_bounds__(256) void pool_reduce_kernel(const float* __restrict__ zpart, int C, int64_t HD,
@@ -395,7 +408,7 @@ hipError_t pool_softmax_wsum(const void* x, int in_bf16, int G, int S, int D, in
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const int C = (S + kPwRows - 1) / kPwRows;
-  hipLaunchKernelGGL(pool_wsum_kernel, dim3(G * C * (D / 256)), dim3(256), 0, s, x, in_bf16, S, D, H, logits, stats,
+  hipLaunchKernelGGL(pool_wsum_kernel, dim3(G * C * (D / 256)), dim3(128), 0, s, x, in_bf16, S, D, H, logits, stats,
                      C, zpart);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
