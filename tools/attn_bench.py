@@ -60,12 +60,12 @@ def long_variants():
     8: without the linear tier for |logit| <= 0.10 cap = round 4's kernel; 16: row sum on the MFMA;
     32: row sum by v_dot2_f32_bf16; 64: unpaired scalar numerator and row sum; 80, 96 combined), at three
     logit scales (std 0.5 / 2 / 6: linear, quadratic / cubic and mixed tiers), interleaved rounds.
-    VP_DIAG_LIB=1 python tools/attn_bench.py long"""
+    VP_DIAG_LIB=1 python tools/attn_bench.py long   (VP_ATTN_VARIANTS=0,8 picks the builds)"""
     dev = torch.device("cuda:0")
     nseq, heads, S = 32, 16, 4096
     D = heads * 64
     st = lambda: torch.cuda.current_stream().cuda_stream
-    variants = (0, 8, 16, 32, 64, 80, 96)
+    variants = tuple(int(v) for v in os.environ.get("VP_ATTN_VARIANTS", "0,8,16,32,64,80,96").split(","))
     for qscale in (0.0625, 0.25, 0.75):
         g = torch.Generator(device=dev).manual_seed(0)
         qkv = torch.randn((nseq * S, 3 * D), generator=g, device=dev)
