@@ -117,6 +117,28 @@ def cpu_baseline(cfg, variables, runs: int = 5, warmups: int = 2) -> dict:
             "runs_s": [round(t, 3) for t in times]}
 
 
+def measured_mfma_peak(device: int, iters: int = 4_000_000, reps: int = 3) -> dict | None:
+    """The bf16 MFMA rate this GPU sustains with every CU issuing back-to-back MFMAs from registers on
+    random operands (tools/peak/mfma_peak.hip): TFLOP/s (median of `reps` launches of
+    ~0.25 s after a warm-up launch) and the in-kernel clock, for both MFMA shapes the kernels use.
+    None if the microbenchmark library is not built (it is measurement only, not the product path)."""
+    import ctypes
+    path = os.path.join(ROOT, "tools", "peak", "libmfma_peak.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    out = {}
+    for shape, key in ((0, "16x16x32"), (1, "32x32x16")):
+        best, med, clk, ms = (ctypes.c_double() for _ in range(4))
+        rc = lib.mfma_peak_run(device, shape, iters if shape == 0 else iters * 2, reps, ctypes.byref(best),
+                               ctypes.byref(med), ctypes.byref(clk), ctypes.byref(ms))
+        if rc != 0:
+            return None
+        out[key] = {"tflops": round(med.value, 1), "tflops_best": round(best.value, 1),
+                    "clock_ghz": round(clk.value, 3), "ms_per_launch": round(ms.value, 1)}
+    return out
+
+
 def load_traffic(path: str, symbol: str, workload: str, src_hash: str):
     """PMC HBM bytes per launch of kernel `symbol` from a traffic record (tools/pmc_summary.py
     --json) -- only when the record was measured on the same sources and workload."""
@@ -439,6 +461,21 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
                          else dom["bytes"] / dom["launches"],
                          "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
                          "traffic_source": tsrc})
+
+    if roofline is not None and rank == 0:
+        # the spec peak beside the peak this GPU sustains (bare MFMAs from registers, all CUs, random data):
+        # the GEMMs issue v_mfma_f32_16x16x32_bf16, the attention kernels v_mfma_f32_32x32x16_bf16
+        pk = measured_mfma_peak(dev.index if dev.index is not None else 0) if roofline["bound"] == "mfma" else None
+        if pk is not None:
+            shape = "16x16x32" if "gemm" in (dom_symbol or "") else "32x32x16"
+            pm = pk[shape]["tflops"]
+            roofline.update({"peak_measured": pm, "frac_measured": round(roofline["achieved"] / pm, 4),
+                             "peak_measured_shape": f"v_mfma_f32_{shape}_bf16",
+                             "peak_measured_clock_ghz": pk[shape]["clock_ghz"],
+                             "peak_measured_all": pk,
+                             "peak_measured_source": "tools/peak/mfma_peak.hip: one 256-thread workgroup per CU, "
+                                                     "back-to-back MFMAs from registers, random bf16, after the "
+                                                     "timed region; median of 3 launches"})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not lvt and not args.standin:

@@ -22,7 +22,11 @@
  *  - vp_forward never allocates, never synchronises: all activations live in the caller's
  *    workspace (size from vp_workspace_bytes); the call is asynchronous on `stream` and
  *    can be captured into a hipGraph.
- *  - A handle is bound to one device and is not thread-safe.
+ *  - A handle is bound to one device and is not thread-safe: calls on one handle must not overlap
+ *    (in particular vp_prepare_geometry / vp_prepare_frames, which add to the handle's cached tables,
+ *    must not run while vp_forward runs on the same handle).  Different handles -- on one device or
+ *    several -- may be driven from different host threads at once: the library's launch state (kernel
+ *    attributes, CU counts) is kept per device and set under a lock.
  */
 #ifndef VIDEOPRISM_HIP_H_
 #define VIDEOPRISM_HIP_H_
@@ -96,8 +100,8 @@ int vp_prepare_geometry(vp_handle* h, int64_t H, int64_t W);
 
 /* Clips of T frames: the temporal positional table resampled to T the way encoders.py:543-553
  * does (_interpolate_emb_1d, :107-130, jax.image.resize 'bilinear', antialiased when shrinking).
- * vp_finalize precomputes T = 1..32; any other T needs one call before vp_forward (allocates;
- * idempotent).  1 <= T <= 2^20. */
+ * vp_finalize precomputes T = 1..32; any other T needs one call before vp_forward (allocates one
+ * [T][D] fp32 table per distinct T, kept until vp_destroy; idempotent).  1 <= T <= 2^20. */
 int vp_prepare_frames(vp_handle* h, int64_t T);
 
 /* Workspace needed by vp_forward for inputs [B, T, H, W, 3]. */
@@ -149,8 +153,9 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
 /* Capped attention over rows qkv[num_seq*S, 3*heads*64] = [q|k|v] (q pre-scaled), writing
  * o[num_seq*S, heads*64].  Replaces DotProductAttention._dot_atten (layers.py:601-661).
  * precision VP_BF16 (S <= 256: the spatial kernel at S == 256, the temporal kernel at S <= 16,
- * the sequence-packed kernel between; S a multiple of 256 without key_pad: the long-sequence kernel of
- * the LvT auxiliary encoder) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL.
+ * the sequence-packed kernel between; any S > 256 without key_pad: the long-sequence kernel of the LvT
+ * auxiliary encoder; S > 256 with key_pad: the online-softmax kernel of vp_op_attention_masked, as the
+ * forward runs it) or VP_F32 (S <= 256).  key_pad: [num_seq*S] or NULL.
  * bf16 with a cap outside (0, 50] (no capping, or one whose unnormalised fp32 numerators could
  * overflow) runs the online-softmax kernel of vp_op_attention_masked, any S. */
 int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, int64_t S,

@@ -219,8 +219,43 @@ def g13_lvt_base_clips():
                         cast_floor_emb=np.stack(cast))
 
 
+# g14: full-depth LvT-Base at frame sizes whose token counts are not multiples of 256 (the reference's
+# FactorizedVideoCLIP runs at any H = W divisible by the patch: encoders.py:505-512 interpolates the spatial
+# table, :846-857 runs the auxiliary encoder over all T*N tokens, :859-885 pools any token count):
+# 252 x 252 (14 x 14 = 196 patches) at T = 16 (3136 auxiliary tokens) and 144 x 144 (8 x 8) at T = 3 (192),
+# B = 3 clips each, two 64-token texts.  fp64 video / text / frame embeddings and similarity, and the bf16
+# cast floor of each clip's video embedding (mode 'wbf16' on bf16-rounded frames, as g13).  ~4 min of oracle.
+G14 = dict(cfg="videoprism_lvt_v1_base", vocabulary_size=1000, param_seed=14, text_seed=44, Q=2, L=64, B=3)
+G14_GEOM = {"s252_t16": (252, 16, 34), "s144_t3": (144, 3, 35)}
+
+
+def g14_video(size, T, seed, B=3):
+    return np.random.default_rng(seed).random((B, T, size, size, 3), dtype=np.float32)
+
+
+def g14_lvt_base_frame_sizes():
+    cfg = dict(models.CONFIGS[G14["cfg"]])
+    cfg["vocabulary_size"] = G14["vocabulary_size"]
+    var = params.synthetic_params(cfg, seed=G14["param_seed"], specs=params.clip_leaf_specs(cfg))
+    ids, pads = g8_text(G14["text_seed"], G14["Q"], G14["L"], cfg["vocabulary_size"])
+    arrays = {k: np.array(v) for k, v in G14.items()}
+    arrays.update(text_token_ids=ids, text_paddings=pads)
+    for tag, (size, T, vseed) in G14_GEOM.items():
+        x = g14_video(size, T, vseed, G14["B"])
+        v, t, out = orc.video_clip(var["params"], cfg, x, ids, pads, "f64", return_intermediate=("frame_embeddings",))
+        arrays[f"{tag}/geometry"] = np.array([size, T, vseed])
+        arrays[f"{tag}/video_emb_f64"] = np.asarray(v, np.float64)
+        arrays[f"{tag}/text_emb_f64"] = np.asarray(t, np.float64)
+        arrays[f"{tag}/similarity_f64"] = np.asarray(v, np.float64) @ np.asarray(t, np.float64).T
+        arrays[f"{tag}/frame_emb_f64"] = np.asarray(out["frame_embeddings"], np.float64)
+        arrays[f"{tag}/cast_floor_emb"] = np.asarray(
+            orc.video_clip(var["params"], cfg, bf16_round(x), None, None, "wbf16")[0], np.float64)
+        print(tag, flush=True)
+    np.savez_compressed(os.path.join(HERE, "g14_lvt_base_frame_sizes.npz"), **arrays)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13"]
+    which = sys.argv[1:] or ["g1", "g2", "g4", "g5", "g6", "g7", "g8", "g9", "g10", "g11", "g12", "g13", "g14"]
     if "g1" in which:
         g1_tiny()
     if "g2" in which:
@@ -241,6 +276,8 @@ if __name__ == "__main__":
         g12_lvt_base_t40()
     if "g13" in which:
         g13_lvt_base_clips()
+    if "g14" in which:
+        g14_lvt_base_frame_sizes()
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

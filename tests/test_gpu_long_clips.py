@@ -71,7 +71,9 @@ def test_long_clip_full_depth_bf16(cuda, which):
     ferr = np.abs(emb[0].reshape(T, -1, emb.shape[-1]).mean(axis=1) - g["frame_mean_f64"]).max()
     print(f"{which} bf16 T={T}: pooled max-abs {perr:.3e}; sampled-token mean-abs {rerr:.3e}; "
           f"frame-mean max-abs {ferr:.3e}")
-    assert perr <= 1e-3 and rerr <= 3e-2
+    # per-frame token means: 2.3-2.9e-2 in the round-5 runs; a fault confined to a few frames (one row of the
+    # resampled temporal table, say) moves one frame's mean by O(|pos-emb|) without moving the pooled vector
+    assert perr <= 1e-3 and rerr <= 3e-2 and ferr <= 5e-2, (perr, rerr, ferr)
 
 
 @pytest.fixture(scope="module")

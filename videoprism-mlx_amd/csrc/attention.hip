@@ -574,16 +574,12 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads, float cap,
                                   const float* key_pad, hipStream_t s, bool blk) {
   if (!(cap > 0.0f)) return hipErrorInvalidValue;
-  static bool attr[4] = {false, false, false, false};
   const int mi = (key_pad ? 1 : 0) + (blk ? 2 : 0);
   const void* fns[4] = {(const void*)attn_spatial_kernel<false, false>, (const void*)attn_spatial_kernel<true, false>,
                         (const void*)attn_spatial_kernel<false, true>, (const void*)attn_spatial_kernel<true, true>};
   const void* fn = fns[mi];
-  if (!attr[mi]) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSpLds);
-    if (e != hipSuccess) return e;
-    attr[mi] = true;
-  }
+  hipError_t e = ensure_dyn_lds(fn, kSpLds);
+  if (e != hipSuccess) return e;
   const dim3 grid(num_seq * heads);
   // frames in reverse order (the producing GEMM's last-written q|k|v rows first): 2.354-2.358 vs
   // 2.400-2.407 ms/step in the forward (round 3, one box, alternating; round 2 measured it neutral)
@@ -628,12 +624,8 @@ hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, 
   const int Sp = S <= 32 ? 32 : S <= 64 ? 64 : S <= 128 ? 128 : 256;
   const int per = kSpS / Sp;
   const void* fn = key_pad ? (const void*)attn_seq_kernel<true> : (const void*)attn_seq_kernel<false>;
-  static bool attr[2] = {false, false};
-  if (!attr[key_pad ? 1 : 0]) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSqLds);
-    if (e != hipSuccess) return e;
-    attr[key_pad ? 1 : 0] = true;
-  }
+  hipError_t e = ensure_dyn_lds(fn, kSqLds);
+  if (e != hipSuccess) return e;
   const int64_t grid = (int64_t)((num_seq + per - 1) / per) * heads;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   VP_NOTE_KERNEL(fn);
@@ -649,15 +641,9 @@ hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, 
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
                          const float* key_pad, hipStream_t s) {
   if (S < 1 || S > kF32MaxS) return hipErrorInvalidValue;
-  static bool attr = false;
   const int lds = (2 * S * 64 + S) * 4 + 16;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)attn_f32_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (2 * kF32MaxS * 64 + kF32MaxS) * 4 + 16);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  hipError_t e = ensure_dyn_lds((const void*)attn_f32_kernel, (2 * kF32MaxS * 64 + kF32MaxS) * 4 + 16);
+  if (e != hipSuccess) return e;
   VP_NOTE_KERNEL(attn_f32_kernel);
   hipLaunchKernelGGL(attn_f32_kernel, dim3(num_seq * heads), dim3(256), lds, s, qkv, o, S, heads, cap, key_pad);
   return hipGetLastError();

@@ -35,8 +35,12 @@ constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 // instead of packed fp32 arithmetic (bitwise the same values); 2 = no quadratic tier; 4 = the row sum
 // one value at a time; 8 = no linear tier; 16 = the row sum on the MFMA (a ones A operand against the
 // bf16 numerators, so the sum of the rounded values P.V uses); 32 = the row sum by v_dot2_f32_bf16 of
-// the bf16 numerator pairs; 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32
-template <int VAR = 0>
+// the bf16 numerator pairs; 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32.
+// TAIL: S % 256 != 0 (S > 256; frame sizes whose T*N is not a multiple of 256, encoders.py:846-857 takes any
+// T*N): nqb = ceil(S / 256) and ceil(S / 64) chunks; a query or key row past S is read from row S - 1 (so
+// every load stays inside the sequence), the numerators of keys past S are zeroed before the row sum and
+// P.V, and queries past S are not stored.  S % 256 == 0 takes TAIL = false: the product instantiation as before
+template <int VAR = 0, bool TAIL = false>
 __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* __restrict__ qkv,
                                                                   bf16_t* __restrict__ o, int S,
                                                                   int heads, int nqb, float cap,
@@ -64,21 +68,23 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
   // cdna_hip_programming.md §5.7 item 1; audited by tools/check_kernels.py)
   bf16x8 qf[4];
   {
-    const bf16_t* qp = base + (int64_t)(q0 + (lane & 31)) * ld + 8 * half;
+    const int qr = TAIL ? min(q0 + (lane & 31), S - 1) : q0 + (lane & 31);
+    const bf16_t* qp = base + (int64_t)qr * ld + 8 * half;
 #pragma unroll
     for (int kd = 0; kd < 4; ++kd)
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[kd]) : "v"(qp + 16 * kd));
   }
   // chunk c -> stage c % 4: wave w loads piece w of the stage's 16 pieces (8 K pieces, then
   // 8 V pieces; a piece = 8 key rows x 128 B = 1 KiB) and piece w + 8
-  const int nchunks = S / kLgChunk;
+  const int nchunks = TAIL ? (S + kLgChunk - 1) / kLgChunk : S / kLgChunk;
   auto issue = [&](int c) {
     char* st = smem + (c & (kLgStages - 1)) * kLgStageBytes;
 #pragma unroll
     for (int isV = 0; isV < 2; ++isV) {
       const int row = w * 8 + (lane >> 3);  // key row within the chunk
       const int ch = (lane & 7) ^ (isV ? swzV(row) : swzK(row));
-      const bf16_t* src = base + (int64_t)(c * kLgChunk + row) * ld + (isV ? 2 * D : D) + ch * 8;
+      const int key = TAIL ? min(c * kLgChunk + row, S - 1) : c * kLgChunk + row;
+      const bf16_t* src = base + (int64_t)key * ld + (isV ? 2 * D : D) + ch * 8;
       __builtin_amdgcn_global_load_lds(VP_GLB_PTR(src), VP_LDS_PTR(st + isV * kLgChunk * 128 + w * 1024),
                                        16, 0, 0);
     }
@@ -134,6 +140,16 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
       capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0, (VAR & 64) != 0>(x, p, c1, c2, cp);
+      if constexpr (TAIL) {
+        // keys past S (the last chunk only): weight 0.  Lane l, value i holds key row
+        // 8 (i / 4) + 4 (l / 32) + i % 4 of the 32-key tile (the 32x32 MFMA output layout)
+        const int kbase = c * kLgChunk + kt * 32 + 4 * half;
+        if (kbase + 28 >= S) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (kbase + 8 * (i >> 2) + (i & 3) >= S) p[i] = 0.0f;
+        }
+      }
       if constexpr ((VAR & 48) != 0) {
         // row sum from the bf16 numerators below
       } else if constexpr ((VAR & 64) != 0) {
@@ -201,6 +217,7 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
     lsum += __shfl_xor(lsum, 32);
   }
   const float inv = 1.0f / lsum;
+  if (TAIL && q0 + (lane & 31) >= S) return;
   bf16_t* op = o + ((int64_t)seq * S + q0 + (lane & 31)) * D + h * 64 + 4 * half;
 #pragma unroll
   for (int g4 = 0; g4 < 4; ++g4) {
@@ -213,25 +230,28 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
   }
 }
 
-template <int VAR>
-hipError_t launch_attn_long(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap, hipStream_t s) {
-  if (S % kLgQ || S < kLgQ || !(cap > 0.0f)) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(attn_long_kernel<VAR>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLgLds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  const int nqb = S / kLgQ;
+template <int VAR, bool TAIL>
+hipError_t launch_attn_long_t(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap, hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(attn_long_kernel<VAR, TAIL>);
+  hipError_t e = ensure_dyn_lds(fn, kLgLds);
+  if (e != hipSuccess) return e;
+  const int nqb = (S + kLgQ - 1) / kLgQ;
   const int64_t grid = (int64_t)num_seq * heads * nqb;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const int xcd_map = grid % 8 == 0 ? 1 : 0;
   const CapPoly cp = make_cap_poly(cap);
-  VP_NOTE_KERNEL(attn_long_kernel<VAR>);
-  hipLaunchKernelGGL(attn_long_kernel<VAR>, dim3((unsigned)grid), dim3(kLgThreads), kLgLds, s, qkv, o, S, heads,
-                     nqb, cap, xcd_map, cp);
+  VP_NOTE_KERNEL(fn);
+  hipLaunchKernelGGL((attn_long_kernel<VAR, TAIL>), dim3((unsigned)grid), dim3(kLgThreads), kLgLds, s, qkv, o, S,
+                     heads, nqb, cap, xcd_map, cp);
   return hipGetLastError();
+}
+
+// S % 256 == 0 (S >= 256) or any S > 256 (TAIL: the prologue's three chunks exist)
+template <int VAR>
+hipError_t launch_attn_long(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads, float cap, hipStream_t s) {
+  if (S < kLgQ || !(cap > 0.0f) || num_seq < 1) return hipErrorInvalidValue;
+  if (S % kLgQ == 0) return launch_attn_long_t<VAR, false>(qkv, o, num_seq, S, heads, cap, s);
+  return launch_attn_long_t<VAR, true>(qkv, o, num_seq, S, heads, cap, s);
 }
 
 }  // namespace

@@ -255,27 +255,13 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_bf16_tn_kernel(
   if (wm == 0) barrier();  // balance the stagger barrier
 }
 
-int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
+int num_cus() { return device_cu_count(); }  // per device (vp_common.h)
 
 template <int EPI>
 hipError_t launch_one(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                       int K, const EpiArgs& ep, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<EPI>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  hipError_t e = ensure_dyn_lds((const void*)gemm_bf16_tn_kernel<EPI>, kGemmLds);
+  if (e != hipSuccess) return e;
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus() ? tiles : num_cus();
   VP_NOTE_KERNEL((gemm_bf16_tn_kernel<EPI>));

@@ -796,27 +796,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int num_cus_w4() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
+int num_cus_w4() { return device_cu_count(); }  // per device (vp_common.h)
 
 template <int EPI, bool NOPAD, bool S3, int ABL = 0, bool AVID = false>
 hipError_t launch_w4(const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M, int N,
                      int K, const EpiArgs& ep, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL, AVID>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsTotal);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  hipError_t e = ensure_dyn_lds((const void*)gemm_bf16_w4_kernel<EPI, NOPAD, S3, ABL, AVID>, kLdsTotal);
+  if (e != hipSuccess) return e;
   const int tiles = (M / BM) * (N / BN);
   const int grid = tiles < num_cus_w4() ? tiles : num_cus_w4();
   const int ngrp = w4_ngrp(M, N, K, grid);

@@ -633,14 +633,16 @@ int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, in
       VP_HIP(attention_masked(qkv, o, 1, (int)num_seq, (int)S, (int)heads, cap, key_pad, 0, s));
     } else if (S == 256)
       VP_HIP(attention_spatial_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)heads, cap, key_pad, s));
-    else if (S > 256 && S % 256 == 0 && !key_pad)
+    else if (S > 256 && !key_pad)  // the auxiliary encoder's kernel (any S; a partial last query block)
       VP_HIP(attention_long_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s));
+    else if (S > 256)  // key paddings beyond 256 keys: the forward's choice (run_stack), the generic kernel
+      VP_HIP(attention_masked(qkv, o, 1, (int)num_seq, (int)S, (int)heads, cap, key_pad, 0, s));
     else if (S >= 1 && S <= 16)
       VP_HIP(attention_temporal_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, key_pad, s));
     else if (S > 16 && S < 256)
       VP_HIP(attention_seq_bf16((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, key_pad, s));
     else
-      return fail(VP_ENOTSUP, "bf16 attention supports S <= 256 or unmasked S % 256 == 0");
+      return fail(VP_EINVAL, "bad S");
   } else if (precision == VP_F32) {
     if (S < 1 || S > 256) return fail(VP_ENOTSUP, "fp32 attention supports S <= 256");
     VP_HIP(attention_f32((const float*)qkv, (float*)o, (int)num_seq, (int)S, (int)heads, cap, key_pad, s));

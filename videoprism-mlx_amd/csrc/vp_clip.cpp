@@ -51,13 +51,14 @@ struct ClipVideoWs {
 ClipVideoWs pool_video_ws(const vp_config& v, int64_t B, int64_t T, int64_t H, int64_t W, size_t inner_bytes,
                           int64_t dp) {
   const int64_t P = v.patch_size, N = (H / P) * (W / P), M = B * T * N;
+  const int64_t Mp = (M + 255) / 256 * 256;  // the auxiliary encoder's GEMM rows (clip_video_chunk)
   const int64_t D = v.model_dim, NH = v.num_heads;
   const size_t es = v.fprop_dtype == VP_BF16 ? 2 : 4;
   const int64_t gc = std::max<int64_t>(B * vp::pool_chunks((int)(T * N)), B * T * vp::pool_chunks((int)N));
   ClipVideoWs L;
   size_t off = 0;
   L.inner = off; off = align256(off + inner_bytes);
-  L.feat = off; off = align256(off + (size_t)M * D * es);
+  L.feat = off; off = align256(off + (size_t)Mp * D * es);
   L.logits = off; off = align256(off + (size_t)M * NH * 4);
   L.stats = off; off = align256(off + (size_t)B * T * NH * 8);
   L.zpart = off; off = align256(off + (size_t)gc * NH * D * 4);
@@ -379,8 +380,10 @@ int clip_video_chunk(vp_clip* c, const void* video, int in_dtype, int64_t B, int
   const int64_t M64 = B * T * N;
   if (M64 > 0x7fffffff) return fail(VP_ENOTSUP, "too many tokens");
   const int M = (int)M64;
-  if (c->cfg.num_auxiliary_layers > 0 && M % (bf ? 256 : 128))
-    return fail(VP_ENOTSUP, "auxiliary encoder GEMMs need B*T*N % 256 == 0 (bf16) / 128 (fp32)");
+  // the auxiliary encoder's GEMM rows: B*T*N padded to the tile (as the vision encoder's, vp_internal.h
+  // padded_rows); the padding rows of feat are zeroed, ride through the row-independent GEMM / LayerNorm
+  // kernels and are never attended to or pooled (every sequence and pooling group is a block of M rows)
+  const int Mp = (int)padded_rows(c->video, M64);
   char* ws = static_cast<char*>(workspace);
   void* feat = ws + L.feat;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -396,18 +399,17 @@ int clip_video_chunk(vp_clip* c, const void* video, int in_dtype, int64_t B, int
   const WsLayout Lv = ws_layout(c->video, B, T, H, W);
   char* wsv = ws + L.inner;
   Fwd f;
-  f.s = s; f.bf = bf; f.M = M; f.D = D; f.NH = NH; f.cap = v.atten_logit_cap;
+  f.s = s; f.bf = bf; f.M = Mp; f.D = D; f.NH = NH; f.cap = v.atten_logit_cap;
   f.hb = wsv + Lv.hbuf; f.big = wsv + Lv.big;
   f.st_part = reinterpret_cast<float*>(wsv + Lv.st_part);
   f.ln_rs = reinterpret_cast<float*>(wsv + Lv.ln_rs);
   f.pf = &c->video->prof;
   // 2. auxiliary encoder over all T*N tokens of each clip (encoders.py:846-857; paddings None)
   if (c->cfg.num_auxiliary_layers > 0) {
-    if (bf) {
-      if (S % 256) return fail(VP_ENOTSUP, "bf16 auxiliary attention needs T*N % 256 == 0");
+    if (Mp > M) VP_HIP(hipMemsetAsync(static_cast<char*>(feat) + (size_t)M * D * es, 0, (size_t)(Mp - M) * D * es, s));
+    if (bf)
       VP_HIP(f.rec(PC_LAYERNORM, 0.0, (double)M * D * 2, [&] {
-        return ln_row_stats((const bf16_t*)feat, M, D, f.ln_rs, s); }));
-    }
+        return ln_row_stats((const bf16_t*)feat, Mp, D, f.ln_rs, s); }));
     rc = f.run_stack(c->aux, feat, (int)B, S, nullptr, v.mlp_dim, PC_ATTN_AUX, ATT_LONG, bf, false);
     if (rc) return rc;
   }

@@ -3,6 +3,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <mutex>
+#include <set>
+#include <utility>
+
 namespace vp {
 
 typedef uint16_t bf16_t;                                            // raw bf16 bits
@@ -223,6 +228,45 @@ __device__ __forceinline__ void lds_read4_b128(bf16x8 (&v)[4], const uint32_t (&
       : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
       : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3])
       : "memory");
+}
+
+// ---- per-device launch state (host) ----
+// The header allows one handle per device, driven from any host thread (include/videoprism_hip.h), so
+// a kernel's dynamic-LDS attribute and the CU count are kept per (device, kernel) / per device, set under
+// a lock the first time, and read lock-free afterwards (a thread-local cache of the pairs already set).
+inline hipError_t ensure_dyn_lds(const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const std::pair<int, const void*> key{dev, fn};
+  thread_local std::set<std::pair<int, const void*>> seen;
+  if (seen.count(key)) return hipSuccess;
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!done.count(key)) {
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+    done.insert(key);
+  }
+  seen.insert(key);
+  return hipSuccess;
+}
+
+// CUs of the current device (256 on MI355X; the persistent GEMM grids are sized by it)
+inline int device_cu_count() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cus[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  if (dev < kMaxDev) {
+    const int c = cus[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  if (dev < kMaxDev) cus[dev].store(n, std::memory_order_relaxed);
+  return n;
 }
 
 // ReLU that keeps a NaN a NaN like jax.nn.relu (text tower ffn_layer1, encoders.py:743): IEEE-754-2019

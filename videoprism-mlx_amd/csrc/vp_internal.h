@@ -555,8 +555,12 @@ struct Fwd {
     ep.out = o; ep.ldo = ldo; ep.bias = bias; ep.resid = resid; ep.ldr = ldo;
     ep.pos = pos; ep.pos_rows = pos_rows; ep.rowpad = rowpad;
     ep.ln_rs = ln_rs; ep.ln_c = lnc; ep.st_part = st_part; ep.st_rows = M;
-    if (bf && small_m && vp::gemm_bf16_small_ok(epi, M, N, K, K, K))
+    if (bf && small_m) {
+      // the text tower's rows are padded to 64 only (clip_text_ws): the 256-row kernels cannot take
+      // them, so an epilogue the small-M kernel lacks is an error here, not a fallback
+      if (!vp::gemm_bf16_small_ok(epi, M, N, K, K, K)) return hipErrorNotSupported;
       return vp::gemm_bf16_small(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wt, K, M, N, K, ep, s);
+    }
     if (bf) return vp::gemm_bf16_auto(epi, (const vp::bf16_t*)A, K, (const vp::bf16_t*)Wt, K, M, N, K, ep, s);
     return vp::gemm_f32(epi, (const float*)A, K, (const float*)Wt, K, M, N, K, ep, s);
   }
@@ -631,9 +635,11 @@ struct Fwd {
         // the bf16 kernels' max-free softmax needs 0 < cap <= kMaxFastCap; cap <= 0 (no capping,
         // layers.py:586-589) or a larger cap runs the online-softmax kernel
         if (bf && !fast_cap(cap)) return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s);
-        if (kind == ATT_LONG) {
-          if (bf) return attention_long_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, s);
-          return attention_masked(big, hb, 0, num_seq, S, NH, cap, nullptr, 0, s);
+        if (kind == ATT_LONG) {  // no masks (encoders.py:855); any T*N
+          if (!bf) return attention_masked(big, hb, 0, num_seq, S, NH, cap, nullptr, 0, s);
+          if (S >= 256) return attention_long_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, s);
+          if (S > 16) return attention_seq_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, nullptr, s);
+          return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, nullptr, s);
         }
         // 16 < S <= 256 (T > 16 frames, other patch grids) on the sequence-packed MFMA kernel; longer sequences
         // on the generic fp32-math kernel
