@@ -130,7 +130,7 @@ def measured_mfma_peak(device: int, iters: int = 4_000_000, reps: int = 3) -> di
     out = {}
     for shape, key in ((0, "16x16x32"), (1, "32x32x16")):
         best, med, clk, ms = (ctypes.c_double() for _ in range(4))
-        rc = lib.mfma_peak_run(device, shape, iters if shape == 0 else iters * 2, reps, ctypes.byref(best),
+        rc = lib.mfma_peak_run(device, shape, iters, reps, ctypes.byref(best),
                                ctypes.byref(med), ctypes.byref(clk), ctypes.byref(ms))
         if rc != 0:
             return None
@@ -282,6 +282,7 @@ def main() -> None:
     ap.add_argument("--frames", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true", help="no per-kernel HIP events")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-peak", action="store_true", help="skip the measured-MFMA-peak microbenchmark")
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic record (default: the newest profiles/traffic_r*_<workload>.json "
@@ -462,7 +463,7 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
                          "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
                          "traffic_source": tsrc})
 
-    if roofline is not None and rank == 0:
+    if roofline is not None and rank == 0 and not args.no_peak:
         # the spec peak beside the peak this GPU sustains (bare MFMAs from registers, all CUs, random data):
         # the GEMMs issue v_mfma_f32_16x16x32_bf16, the attention kernels v_mfma_f32_32x32x16_bf16
         pk = measured_mfma_peak(dev.index if dev.index is not None else 0) if roofline["bound"] == "mfma" else None

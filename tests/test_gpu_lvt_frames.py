@@ -136,8 +136,9 @@ def test_lvt_base_frame_sizes_full_depth(cuda, g14, tag, B, bf16):
     es = np.abs(v @ t.T - g[f"{tag}/similarity_f64"][:B]).max()
     ef = np.abs(f - g[f"{tag}/frame_emb_f64"][:B]).max()
     floor = np.abs(g[f"{tag}/cast_floor_emb"][:B] - g[f"{tag}/video_emb_f64"][:B]).max(axis=-1)
-    print(f"LvT-B {tag} B={B} {'bf16' if bf16 else 'f32'}: video {np.array2string(ev, precision=3)} "
-          f"(cast floor {np.array2string(floor, precision=3)}) text {et:.3e} similarity {es:.3e} frames {ef:.3e}")
+    fmt = lambda a: "[" + " ".join(f"{v:.3e}" for v in a) + "]"  # noqa: E731
+    print(f"LvT-B {tag} B={B} {'bf16' if bf16 else 'f32'}: video {fmt(ev)} (cast floor {fmt(floor)}) text {et:.3e} "
+          f"similarity {es:.3e} frames {ef:.3e}")
     if bf16:
         vbar = np.maximum(1e-3, 1.1 * floor)
         assert np.all(ev <= vbar) and et <= 1e-3 and es <= 1e-3 and ef <= 2e-3, (ev, floor, et, es, ef)

@@ -20,6 +20,19 @@ hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const
   return hipErrorInvalidValue;
 }
 
+hipError_t gemm_bf16_w4_ffn1_abl(int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K, const EpiArgs& ep,
+                                 hipStream_t s) {
+  if (K % BK || M % BM || N % BN) return hipErrorInvalidValue;
+  switch (abl) {
+    case 0: return launch_w4<EPI_GELU_BF16_LN_BLK, true, false, 0>(A, K, W, K, M, N, K, ep, s);
+    case 2: return launch_w4<EPI_GELU_BF16_LN_BLK, true, false, 2>(A, K, W, K, M, N, K, ep, s);
+    case 4: return launch_w4<EPI_GELU_BF16_LN_BLK, true, false, 4>(A, K, W, K, M, N, K, ep, s);
+    case 8: return launch_w4<EPI_GELU_BF16_LN_BLK, true, false, 8>(A, K, W, K, M, N, K, ep, s);
+    case 14: return launch_w4<EPI_GELU_BF16_LN_BLK, true, false, 14>(A, K, W, K, M, N, K, ep, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 // the fused temporal attention launches (which 0: EPI_QK_TATTN_LN, 1: EPI_V_TATTN_LN) with ABL bits
 // (8: no epilogue, prices it)
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,

@@ -9,6 +9,10 @@ namespace vp {
 // K-loop, 4 = no staging loads after the prologue, 8 = no epilogue, EPI_BF16 (S3 when s3 != 0)
 hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t ldw, int M,
                             int N, int K, const EpiArgs& ep, hipStream_t s);
+// the product ffn_layer1 launch (EPI_GELU_BF16_LN_BLK, no padded rows, 2-stage) with ABL bits: 2 = no ds_reads,
+// 4 = no staging loads, 8 = no epilogue (prices the LN fold + GELU against the K-loop)
+hipError_t gemm_bf16_w4_ffn1_abl(int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K, const EpiArgs& ep,
+                                 hipStream_t s);
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
                                   const EpiArgs& ep, hipStream_t s);
 

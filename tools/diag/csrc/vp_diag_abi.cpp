@@ -22,6 +22,17 @@ int vp_dev_gemm_w4_abl(int abl, int s3, const void* A, const void* W, int64_t M,
   return VP_OK;
 }
 
+// the product ffn_layer1 launch (EPI_GELU_BF16_LN_BLK) with ablation bits; out [M/16][N/32][16][32] bf16
+int vp_dev_gemm_ffn1_abl(int abl, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
+                         const float* bias, const float* ln_rs, const float* ln_c, void* stream) {
+  using namespace vp;
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias; ep.ln_rs = ln_rs; ep.ln_c = ln_c;
+  VP_HIP(gemm_bf16_w4_ffn1_abl(abl, (const bf16_t*)A, (const bf16_t*)W, (int)M, (int)N, (int)K, ep,
+                               static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // the fused temporal attention launches with ablation bits (vp_dev_gemm_tattn of the product ABI + abl)
 int vp_dev_gemm_tattn_abl(int which, int abl, const void* A, const void* W, int64_t M, int64_t K, void* out,
                           const float* bias, const float* ln_rs, const float* ln_c, const void* p, int64_t heads,

@@ -4,8 +4,8 @@
 //
 // Every CU runs one 256-thread workgroup (one wave per SIMD); each wave keeps its A / B fragments (random
 // bf16 from a per-lane hash: the chip holds a lower clock on random operands than on zeros,
-// MI355X_MICROARCH.md "DVFS give-back") and NACC independent accumulators in registers and issues
-// `iters` x NACC back-to-back MFMAs of one shape: v_mfma_f32_16x16x32_bf16 (the GEMMs' instruction) or
+// MI355X_MICROARCH.md "DVFS give-back") and independent accumulators in registers (8 of 16x16, 4 of 32x32) and
+// issues `iters` x 8 / 4 back-to-back MFMAs of one shape: v_mfma_f32_16x16x32_bf16 (the GEMMs' instruction) or
 // v_mfma_f32_32x32x16_bf16 (the attention kernels').  TFLOP/s = FLOPs / event time of the launch.
 // Wave 0 of each workgroup stamps s_memtime (shader clock) and s_memrealtime (100 MHz) around its loop
 // into a buffer of its own (nothing reads it back on the device): clock = d(memtime) / d(realtime) x 100 MHz.
@@ -39,7 +39,6 @@ __device__ __forceinline__ bf16x8 rand_frag(uint32_t seed) {
 
 template <int SHAPE>  // 0: 16x16x32, 1: 32x32x16
 __global__ __launch_bounds__(256) void mfma_peak_kernel(int iters, float* sink, unsigned long long* stamps) {
-  constexpr int NACC = 8;
   const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
   const bf16x8 a = rand_frag(gid * 2u + 1u), b = rand_frag(gid * 2u + 2u);
   unsigned long long t0 = 0, r0 = 0;
@@ -47,29 +46,31 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(int iters, float* sink, 
     t0 = __builtin_amdgcn_s_memtime();
     r0 = __builtin_amdgcn_s_memrealtime();
   }
+  // the MFMAs as asm statements: the compiler, given an accumulator array in a loop, rotates it through
+  // AGPR copies between iterations (measured 874 TF); each statement here is exactly one MFMA on a fixed
+  // register quad / block, and an accumulator recurs every NACC MFMAs (128 cycles, past any latency)
   float s = 0.0f;
   if constexpr (SHAPE == 0) {
-    f32x4 acc[NACC];
-#pragma unroll
-    for (int i = 0; i < NACC; ++i) acc[i] = f32x4{(float)i, 0.f, 0.f, 0.f};  // distinct chains (no CSE)
+    f32x4 a0 = {0.f}, a1 = {1.f}, a2 = {2.f}, a3 = {3.f}, a4 = {4.f}, a5 = {5.f}, a6 = {6.f}, a7 = {7.f};
+#pragma unroll 1
     for (int it = 0; it < iters; ++it) {
-#pragma unroll
-      for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+#define VP_M16(acc) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
+      VP_M16(a0); VP_M16(a1); VP_M16(a2); VP_M16(a3); VP_M16(a4); VP_M16(a5); VP_M16(a6); VP_M16(a7);
+#undef VP_M16
     }
-#pragma unroll
-    for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    const f32x4 t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    s = t[0] + t[1] + t[2] + t[3];
   } else {
-    f32x16 acc[NACC / 2];
-#pragma unroll
-    for (int i = 0; i < NACC / 2; ++i) acc[i] = f32x16{(float)i};  // distinct chains (no CSE)
+    f32x16 a0 = {0.f}, a1 = {1.f}, a2 = {2.f}, a3 = {3.f};
+#pragma unroll 1
     for (int it = 0; it < iters; ++it) {
-#pragma unroll
-      for (int i = 0; i < NACC / 2; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+#define VP_M32(acc) asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b))
+      VP_M32(a0); VP_M32(a1); VP_M32(a2); VP_M32(a3);
+#undef VP_M32
     }
+    const f32x16 t = a0 + a1 + a2 + a3;
 #pragma unroll
-    for (int i = 0; i < NACC / 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) s += acc[i][j];
+    for (int j = 0; j < 16; ++j) s += t[j];
   }
   if (threadIdx.x == 0) {
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -101,8 +102,8 @@ int mfma_peak_run(int device, int shape, int iters, int reps, double* tflops_bes
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  // FLOPs per MFMA: 2 * 16 * 16 * 32 = 2 * 32 * 32 * 16 = 16384; 8 (16x16) or 4 (32x32) per iteration
-  const double flops = (double)cus * 4 * iters * (shape == 0 ? 8.0 : 4.0) * 16384.0;
+  // FLOPs per MFMA: 2 * 16 * 16 * 32 = 16384 (8 per iteration) or 2 * 32 * 32 * 16 = 32768 (4 per iteration)
+  const double flops = (double)cus * 4 * iters * (shape == 0 ? 8.0 * 16384.0 : 4.0 * 32768.0);
   std::vector<double> tf;
   for (int r = 0; r <= reps && e == hipSuccess; ++r) {
     hipEventRecord(a, nullptr);

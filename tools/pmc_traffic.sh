@@ -3,11 +3,11 @@
 # group (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass), then the per-symbol
 # traffic record bench.py reads for roofline.traffic.
 # Usage (on the GPU box, from the repo root): tools/pmc_traffic.sh OUTDIR WORKLOAD [RECORD]
-#   RECORD defaults to profiles/traffic_r05_WORKLOAD.json
+#   RECORD defaults to profiles/traffic_r06_WORKLOAD.json
 set -e
 OUT=$(realpath -m "$1")
 WL=${2:-base}
-REC=${3:-profiles/traffic_r05_${WL}.json}
+REC=${3:-profiles/traffic_r06_${WL}.json}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -15,7 +15,7 @@ i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d "$OUT/p$i" -o pmc -- \
-    python3 "$ROOT/bench.py" --workload "$WL" --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/p$i.log" 2>&1
+    python3 "$ROOT/bench.py" --workload "$WL" --steps 2 --warmup 1 --no-cpu-baseline --no-peak > "$OUT/p$i.log" 2>&1
 done
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" --json "$REC" "$WL" > "$OUT/summary.txt"
 cat "$OUT/summary.txt"

@@ -153,6 +153,8 @@ _DIAG_SIGNATURES = {
                                       c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_w4_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
                                    c_void_p, c_void_p]),
+    "vp_dev_gemm_ffn1_abl": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None
@@ -208,7 +210,12 @@ def check(rc: int) -> None:
 
 
 def call(name: str, *args) -> None:
-    check(getattr(load(), name)(*args))
+    fn = getattr(load(), name)
+    # an undeclared signature would pass Python ints as 32-bit c_int: a device pointer truncated that way
+    # is an illegal address on the GPU, so every entry point called here must be declared
+    if getattr(fn, "argtypes", None) is None:
+        raise TypeError(f"{name}: no ctypes signature declared in _native.py")
+    check(fn(*args))
 
 
 # ---------------------------------------------------------------------------------------
