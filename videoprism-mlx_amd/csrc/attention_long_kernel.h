@@ -35,7 +35,8 @@ constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 // instead of packed fp32 arithmetic (bitwise the same values); 2 = no quadratic tier; 4 = the row sum
 // one value at a time; 8 = no linear tier; 16 = the row sum on the MFMA (a ones A operand against the
 // bf16 numerators, so the sum of the rounded values P.V uses); 32 = the row sum by v_dot2_f32_bf16 of
-// the bf16 numerator pairs; 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32.
+// the bf16 numerator pairs; 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32; 128 = the LIN
+// tier in packed pairs; 256 = s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4).
 // TAIL: S % 256 != 0 (S > 256; frame sizes whose T*N is not a multiple of 256, encoders.py:846-857 takes any
 // T*N): nqb = ceil(S / 256) and ceil(S / 64) chunks; a query or key row past S is read from row S - 1 (so
 // every load stays inside the sequence), the numerators of keys past S are zeroed before the row sum and
@@ -106,6 +107,9 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
   const int g = lane >> 4;
   const int li = lane & 15;
   const int trq = li >> 2, trp = li & 3;
+  if constexpr ((VAR & 256) != 0) {
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
+  }
 
 #pragma unroll 1
   for (int c = 0; c < nchunks; ++c) {
@@ -139,7 +143,8 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
-      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0, (VAR & 64) != 0>(x, p, c1, c2, cp);
+      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0, (VAR & 64) != 0, (VAR & 128) != 0>(x, p, c1, c2,
+                                                                                                     cp);
       if constexpr (TAIL) {
         // keys past S (the last chunk only): weight 0.  Lane l, value i holds key row
         // 8 (i / 4) + 4 (l / 32) + i % 4 of the 32-key tile (the 32x32 MFMA output layout)
@@ -253,6 +258,7 @@ hipError_t launch_attn_long(const bf16_t* qkv, bf16_t* o, int num_seq, int S, in
   if (S % kLgQ == 0) return launch_attn_long_t<VAR, false>(qkv, o, num_seq, S, heads, cap, s);
   return launch_attn_long_t<VAR, true>(qkv, o, num_seq, S, heads, cap, s);
 }
+
 
 }  // namespace
 

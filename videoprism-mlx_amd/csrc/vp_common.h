@@ -111,17 +111,29 @@ __device__ __forceinline__ float fma_s(float a, float b, float c) {
   return r;
 }
 
-// SCALAR (A/B builds): the LIN / QUAD tiers in unpaired scalar fp32 (the same IEEE operations)
-template <bool PACKED = true, bool QUAD = false, bool LIN = false, bool SCALAR = false>
+// SCALAR (A/B builds): the LIN / QUAD tiers in unpaired scalar fp32 (the same IEEE operations); PKLIN (A/B
+// builds): the LIN tier in packed pairs (the same IEEE operations, half the instructions)
+template <bool PACKED = true, bool QUAD = false, bool LIN = false, bool SCALAR = false, bool PKLIN = false>
 __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
   float mx = 0.0f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
   if (LIN && __builtin_amdgcn_ballot_w64(mx > cp.x2) == 0) {
+    if constexpr (PKLIN) {
+      typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if constexpr (SCALAR) p[i] = __builtin_amdgcn_exp2f(mul_s(x[i], fma_s(cp.l1, mul_s(x[i], x[i]), cp.l0)));
-      else p[i] = __builtin_amdgcn_exp2f(x[i] * fmaf(cp.l1, x[i] * x[i], cp.l0));
+      for (int i = 0; i < 16; i += 2) {
+        const f2_t xv = {x[i], x[i + 1]};
+        const f2_t g = xv * __builtin_elementwise_fma(f2_t(cp.l1), xv * xv, f2_t(cp.l0));
+        p[i] = __builtin_amdgcn_exp2f(g.x);
+        p[i + 1] = __builtin_amdgcn_exp2f(g.y);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if constexpr (SCALAR) p[i] = __builtin_amdgcn_exp2f(mul_s(x[i], fma_s(cp.l1, mul_s(x[i], x[i]), cp.l0)));
+        else p[i] = __builtin_amdgcn_exp2f(x[i] * fmaf(cp.l1, x[i] * x[i], cp.l0));
+      }
     }
   } else if (QUAD && __builtin_amdgcn_ballot_w64(mx > cp.x1) == 0) {
 #pragma unroll
