@@ -180,3 +180,28 @@ def test_temporal_beyond_256_frames(cuda, bf16, T, size, padded):
         err = np.abs(emb - ref).max()
         print(f"T={T} {size}x{size} padded={padded} f32: max-abs {err:.3e}")
         assert err <= 1e-5
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("size,T", [(36, 3), (108, 5), (90, 12)])
+def test_lvt_reduced_depth_small_grids(cuda, size, T, bf16):
+    """LvT-Base dims, 1 + 1 vision / 1 auxiliary / 1 text layer, at grids of 2x2 (12 auxiliary tokens: the
+    temporal kernel), 6x6 (180: the sequence kernel) and 5x5 at T = 12 (300: the long kernel's partial
+    block), B = 2, vs the fp64 oracle on the fly."""
+    cfg = dict(models.CONFIGS["videoprism_lvt_v1_base"], vocabulary_size=100, num_spatial_layers=1,
+               num_temporal_layers=1, num_auxiliary_layers=1, num_unimodal_layers=1)
+    var = params.synthetic_params(cfg, size + T, specs=params.clip_leaf_specs(cfg))
+    video = np.random.default_rng(size).random((2, T, size, size, 3), dtype=np.float32)
+    ids = np.random.default_rng(T).integers(0, 100, (2, 9)).astype(np.int32)
+    pads = np.zeros((2, 9), np.float32)
+    pads[1, 4:] = 1.0
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedVideoCLIP(**cfg),
+                         fprop_dtype=torch.bfloat16 if bf16 else None)
+    v, t, out = m.apply(var, video, ids, pads, return_intermediate=("frame_embeddings",))
+    rv, rt, rout = orc.video_clip(var["params"], cfg, video, ids, pads, "f64", return_intermediate=("frame_embeddings",))
+    ev, et = np.abs(v - rv).max(), np.abs(t - rt).max()
+    ef = np.abs(out["frame_embeddings"] - rout["frame_embeddings"]).max()
+    print(f"LvT-B 1+1/1/1 {size}x{size} T={T} ({T * (size // 18) ** 2} aux tokens) {'bf16' if bf16 else 'f32'}: "
+          f"video {ev:.3e} frames {ef:.3e} text {et:.3e}")
+    tol = 2e-3 if bf16 else 2e-5
+    assert ev <= tol and ef <= tol and et <= tol, (ev, ef, et)
