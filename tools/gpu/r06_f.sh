@@ -12,7 +12,8 @@ test -f videoprism-mlx_amd/videoprism/libvideoprism_hip.so || { echo "product li
 step hash_new 300 bash -c "python -u tools/ab_forward_hash.py > $O/hash_new.json 2>$O/hash_new.err"
 step hash_r05 300 bash -c "python -u tools/ab_forward_hash.py .ab/r05 > $O/hash_r05.json 2>$O/hash_r05.err"
 step ffn1_split 300 bash -c "python -u tools/ffn1_split.py > $O/ffn1_split.log 2>&1"
-step ab 900 bash -c "bash tools/gpu/ab_bench.sh pre 3 > $O/ab.log 2>&1"
+step ab_pre 600 bash -c "bash tools/gpu/ab_bench.sh pre 3 > $O/ab_pre.log 2>&1"
+step ab_blk 600 bash -c "bash tools/gpu/ab_bench.sh blk 3 > $O/ab_blk.log 2>&1"
 echo "[$(date +%T)] tests start"
 timeout -k 10 900 bash -c "python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > $O/gputest.log 2>&1"
 rc=$?; echo "[$(date +%T)] tests rc=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc

@@ -68,9 +68,7 @@ hipError_t gemm_bf16_w4_launch(int epi, const bf16_t* A, int64_t lda, const bf16
     // for ffn_layer1, A blocked for ffn_layer2 (lda = K, K % 64 == 0)
     case EPI_GELU_BF16_LN_BLK:
       if (N % 32 || ldw != K) return hipErrorInvalidValue;
-      // the 2-stage form keeps the LN-fold constants of all N columns in LDS (gemm_w4_kernel.h kLcAll: N <= 4096)
-      if (!ep.rowpad && N <= 4096) return launch_w4<EPI_GELU_BF16_LN_BLK, true, S2>(A, lda, W, ldw, M, N, K, ep, s);
-      if (!ep.rowpad) return launch_w4<EPI_GELU_BF16_LN_BLK, true, S3>(A, lda, W, ldw, M, N, K, ep, s);
+      if (!ep.rowpad) return launch_w4<EPI_GELU_BF16_LN_BLK, true, S2>(A, lda, W, ldw, M, N, K, ep, s);
       return launch_w4<EPI_GELU_BF16_LN_BLK, false, S2>(A, lda, W, ldw, M, N, K, ep, s);
     case EPI_BF16_LN_BLK:
       if (N % 32 || ldw != K) return hipErrorInvalidValue;

@@ -251,21 +251,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
         fw[set][nt], fa[set][mt], zero ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[nt][mt], 0, 0, 0);
   };
 
-  // ---- row-blocked epilogues on the 2-stage kernel (ffn_layer1): the LN-fold constants c and b' of ALL N
-  // columns go to the epilogue region (free in this configuration) once, here, so no epilogue issues a
-  // global load -- its value would be waited for behind the next tile's K-stream loads (vmcnt retires in
-  // issue order).  N <= 4096 (32 KiB: the launcher sends wider launches to the S3 form, which loads the
-  // wave's 128 columns per tile).  (Visible to the other waves after the first h1's barrier; the first h0's
-  // lgkmcnt(0) retires the writes.)
-  constexpr bool kLcAll = EpiTraits<EPI>::kBlkOut && !S3 && NOPAD;  // (with padded rows: register room)
-  if constexpr (kLcAll) {
-    float* lcs = reinterpret_cast<float*>(smem + kLds);
-    for (int i = (int)threadIdx.x * 4; i < N; i += kThreads * 4) {
-      *reinterpret_cast<float4*>(lcs + i) = *reinterpret_cast<const float4*>(ep.ln_c + i);
-      *reinterpret_cast<float4*>(lcs + N + i) = *reinterpret_cast<const float4*>(ep.bias + i);
-    }
-  }
-
   // ---- prologue: K-tiles 0, 1 into buffers 0, 1; fragments of (0, h0)
 #pragma unroll
   for (int p = 0; p < 16; ++p) stage_piece(0, p);
@@ -309,23 +294,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
   // 16 loads of K-tile g+2 into buffer cb.  DEFER (the fused temporal launches' last K-tile of a
   // tile): the reads of set 0 are left to the end of the epilogue, so their 64 registers are free in it
   // EARLY (kEarly's last K-tile): 4 residual loads were issued after this K-tile's h0 pieces
-  // AFTER (the first K-tile of a tile after a row-blocked epilogue): that epilogue's 32 block stores are younger
-  // than the K-tile pieces this wait is for, so they stay in flight (vmcnt retires in issue order; every
-  // other op issued since -- the tile's row statistics, the h0 A pieces on S3 -- only adds younger ones)
-  auto h1 = [&](int cb, auto DEFER, auto EARLY, bool after) {
+  auto h1 = [&](int cb, auto DEFER, auto EARLY) {
     constexpr bool defer = decltype(DEFER)::value;
     constexpr bool early = decltype(EARLY)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     // S3: K-tile g+1 has landed once all but this K-tile's h0 A pieces (of g+2) are done
-    if constexpr (S3 && early) {
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else if constexpr (S3) {
-      if (after) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      if (after) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if constexpr (S3 && early) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (S3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sched_fence();
     mfma(1, 0, false);
     mfma(1, 1, false);
@@ -414,14 +390,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
     }
     if constexpr (EpiTraits<EPI>::kVAttn || EpiTraits<EPI>::kQkAttn) {  // last K-tile peeled (K >= 2 BK)
       h0(g & 1, true);
-      h1(g & 1, std::false_type{}, std::false_type{}, false);
+      h1(g & 1, std::false_type{}, std::false_type{});
       ++g;
       for (int kt = 1; kt < nk - 1; ++kt, ++g) {
         h0(g & 1, false);
-        h1(g & 1, std::false_type{}, std::false_type{}, false);
+        h1(g & 1, std::false_type{}, std::false_type{});
       }
       h0(g & 1, false);
-      h1(g & 1, std::true_type{}, std::false_type{}, false);
+      h1(g & 1, std::true_type{}, std::false_type{});
       ++g;
     } else {
       auto fetch_raw = [&](int bsel, int mt) {
@@ -434,21 +410,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
                 nh * 64 + es * 8);
       };
       h0(g & 1, true);
-      h1(g & 1, std::false_type{}, std::false_type{}, EpiTraits<EPI>::kBlkOut && !(ABL & 8) && j > 0);
+      h1(g & 1, std::false_type{}, std::false_type{});
       ++g;
       if constexpr (kEarly) {  // last K-tile peeled (the launcher checks K >= 2 BK)
         for (int kt = 1; kt < nk - 1; ++kt, ++g) {
           h0(g & 1, false);
-          h1(g & 1, std::false_type{}, std::false_type{}, false);
+          h1(g & 1, std::false_type{}, std::false_type{});
         }
         h0(g & 1, false);
         fetch_raw(0, 0);
-        h1(g & 1, std::false_type{}, std::true_type{}, false);
+        h1(g & 1, std::false_type{}, std::true_type{});
         ++g;
       } else {
         for (int kt = 1; kt < nk; ++kt, ++g) {
           h0(g & 1, false);
-          h1(g & 1, std::false_type{}, std::false_type{}, false);
+          h1(g & 1, std::false_type{}, std::false_type{});
         }
       }
     }
@@ -480,22 +456,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_w4_kernel(
       for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) asm volatile("" : "+a"(acc[nt][mt]));
-      // the LN-fold constants of the wave's 128 W rows: c at lcc, b' at lcb -- from the all-columns copy the
-      // prologue made (lcall), else loaded here into the wave's scratch (c at +0, b' at +512)
-      const char* lcc = kLcAll ? smem + kLds + 4 * n0 : scr;
-      const char* lcb = kLcAll ? smem + kLds + 4 * (N + n0) : scr + 512;
-      if constexpr (!kLcAll) {
+      char* lc = scr;  // c at +0, b' at +512 (the wave's 128 W rows)
+      {
         const float* src = (lid < 32 ? ep.ln_c : ep.bias) + n0 + 4 * (lid & 31);
-        *reinterpret_cast<float4*>(scr + (lid < 32 ? 0 : 512) + 16 * (lid & 31)) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(lc + (lid < 32 ? 0 : 512) + 16 * (lid & 31)) = *reinterpret_cast<const float4*>(src);
       }
       const int64_t nblk = N >> 5;
       bf16_t* outp = static_cast<bf16_t*>(ep.out);
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        const float4 c0 = *reinterpret_cast<const float4*>(lcc + 4 * (32 * p + 4 * g4));
-        const float4 c1 = *reinterpret_cast<const float4*>(lcc + 4 * (32 * p + 16 + 4 * g4));
-        const float4 b0 = *reinterpret_cast<const float4*>(lcb + 4 * (32 * p + 4 * g4));
-        const float4 b1 = *reinterpret_cast<const float4*>(lcb + 4 * (32 * p + 16 + 4 * g4));
+        const float4 c0 = *reinterpret_cast<const float4*>(lc + 4 * (32 * p + 4 * g4));
+        const float4 c1 = *reinterpret_cast<const float4*>(lc + 4 * (32 * p + 16 + 4 * g4));
+        const float4 b0 = *reinterpret_cast<const float4*>(lc + 512 + 4 * (32 * p + 4 * g4));
+        const float4 b1 = *reinterpret_cast<const float4*>(lc + 512 + 4 * (32 * p + 16 + 4 * g4));
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
           f32x2_t v[4];
