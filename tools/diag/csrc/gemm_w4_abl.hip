@@ -33,6 +33,21 @@ hipError_t gemm_bf16_w4_ffn1_abl(int abl, const bf16_t* A, const bf16_t* W, int 
   return hipErrorInvalidValue;
 }
 
+// the product ffn_layer2 launch (EPI_RESID_FFN_BF16_ST_BLK: A = the row-blocked hidden, S3, residual + row
+// statistics) with ABL bits as above
+hipError_t gemm_bf16_w4_ffn2_abl(int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K, const EpiArgs& ep,
+                                 hipStream_t s) {
+  if (K % BK || M % BM || N % BN || K < 2048) return hipErrorInvalidValue;
+  switch (abl) {
+    case 0: return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, true, 0>(A, K, W, K, M, N, K, ep, s);
+    case 2: return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, true, 2>(A, K, W, K, M, N, K, ep, s);
+    case 4: return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, true, 4>(A, K, W, K, M, N, K, ep, s);
+    case 8: return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, true, 8>(A, K, W, K, M, N, K, ep, s);
+    case 14: return launch_w4<EPI_RESID_FFN_BF16_ST_BLK, false, true, 14>(A, K, W, K, M, N, K, ep, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 // the fused temporal attention launches (which 0: EPI_QK_TATTN_LN, 1: EPI_V_TATTN_LN) with ABL bits
 // (8: no epilogue, prices it)
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,

@@ -13,6 +13,8 @@ hipError_t gemm_bf16_w4_abl(int abl, int s3, const bf16_t* A, int64_t lda, const
 // 4 = no staging loads, 8 = no epilogue (prices the LN fold + GELU against the K-loop)
 hipError_t gemm_bf16_w4_ffn1_abl(int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K, const EpiArgs& ep,
                                  hipStream_t s);
+hipError_t gemm_bf16_w4_ffn2_abl(int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K, const EpiArgs& ep,
+                                 hipStream_t s);
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
                                   const EpiArgs& ep, hipStream_t s);
 

@@ -33,6 +33,18 @@ int vp_dev_gemm_ffn1_abl(int abl, const void* A, const void* W, int64_t M, int64
   return VP_OK;
 }
 
+// the product ffn_layer2 launch with ablation bits: A [M/16][K/32][16][32] bf16 (row-blocked), out = resid
+// [M][N] bf16 in place, st_part [N/128][M][2]
+int vp_dev_gemm_ffn2_abl(int abl, const void* A, const void* W, int64_t M, int64_t N, int64_t K, void* out,
+                         const float* bias, float* st_part, void* stream) {
+  using namespace vp;
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = out; ep.ldr = N; ep.st_part = st_part; ep.st_rows = M;
+  VP_HIP(gemm_bf16_w4_ffn2_abl(abl, (const bf16_t*)A, (const bf16_t*)W, (int)M, (int)N, (int)K, ep,
+                               static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 // the fused temporal attention launches with ablation bits (vp_dev_gemm_tattn of the product ABI + abl)
 int vp_dev_gemm_tattn_abl(int which, int abl, const void* A, const void* W, int64_t M, int64_t K, void* out,
                           const float* bias, const float* ln_rs, const float* ln_c, const void* p, int64_t heads,

@@ -155,6 +155,8 @@ _DIAG_SIGNATURES = {
                                    c_void_p, c_void_p]),
     "vp_dev_gemm_ffn1_abl": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_void_p]),
+    "vp_dev_gemm_ffn2_abl": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
 }
 
 _lib = None
