@@ -205,3 +205,31 @@ def test_lvt_reduced_depth_small_grids(cuda, size, T, bf16):
           f"video {ev:.3e} frames {ef:.3e} text {et:.3e}")
     tol = 2e-3 if bf16 else 2e-5
     assert ev <= tol and ef <= tol and et <= tol, (ev, ef, et)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bf16", [False, True])
+def test_lvt_large_dims_252_uint8_padded(cuda, bf16):
+    """LvT-Large dims (D 1024, 16 heads), 1 + 1 vision / 2 auxiliary / 1 text layer, 252 x 252 uint8 frames (the
+    /255 ingest), T = 7 with the last two frames of clip 1 padded (the vision encoder masks them; the auxiliary
+    encoder and the poolers see no paddings, encoders.py:846-885): 1372 auxiliary tokens (partial last block)."""
+    cfg = dict(models.CONFIGS["videoprism_lvt_v1_large"], vocabulary_size=100, num_spatial_layers=1,
+               num_temporal_layers=1, num_auxiliary_layers=2, num_unimodal_layers=1)
+    var = params.synthetic_params(cfg, 31, specs=params.clip_leaf_specs(cfg))
+    frames = np.random.default_rng(31).integers(0, 256, (2, 7, 252, 252, 3), dtype=np.uint8)
+    fp = np.zeros((2, 7), np.float32)
+    fp[1, 5:] = 1.0
+    ids = np.random.default_rng(32).integers(0, 100, (3, 12)).astype(np.int32)
+    pads = np.zeros((3, 12), np.float32)
+    pads[2, 6:] = 1.0
+    m = models.get_model(None, model_fn=lambda: encoders.FactorizedVideoCLIP(**cfg),
+                         fprop_dtype=torch.bfloat16 if bf16 else None)
+    v, t, out = m.apply(var, frames, ids, pads, frame_paddings=fp, return_intermediate=("frame_embeddings",))
+    video = frames.astype(np.float32) / np.float32(255.0)  # video_utils.py:94
+    rv, rt, rout = orc.video_clip(var["params"], cfg, video, ids, pads, "f64",
+                                  return_intermediate=("frame_embeddings",), frame_paddings=fp)
+    ev, et = np.abs(v - rv).max(), np.abs(t - rt).max()
+    ef = np.abs(out["frame_embeddings"] - rout["frame_embeddings"]).max()
+    print(f"LvT-L dims 252x252 uint8 T=7 padded {'bf16' if bf16 else 'f32'}: video {ev:.3e} frames {ef:.3e} text {et:.3e}")
+    tol = 2e-3 if bf16 else 2e-5
+    assert ev <= tol and ef <= tol and et <= tol, (ev, ef, et)
