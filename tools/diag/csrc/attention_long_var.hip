@@ -4,7 +4,8 @@
 // quadratic tier for small logits, 4 = the row sum one value at a time, 8 = without the linear tier
 // (round 4's product kernel), 16 = the row sum on the MFMA, 32 = the row sum by v_dot2_f32_bf16,
 // 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32, 128 = the LIN tier packed, 256 = s_setprio 1
-// for waves 4-7 (bits combine: 6 = round 3's kernel).
+// for waves 4-7, 1024 = round 5's chunk loop (addresses per tile; the product unrolls over the LDS stages)
+// (bits combine: 6 = round 3's kernel).
 #include "attention_long_kernel.h"
 #include "attention_long_pp.h"
 
@@ -27,6 +28,7 @@ extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int6
   if (var == 128) e = launch_attn_long<128>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 256) e = launch_attn_long<256>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 384) e = launch_attn_long<384>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
+  if (var == 1024) e = launch_attn_long<1024>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   // 512 + bits: the two-waves-per-SIMD alternating kernel (attn_long_pp_kernel) with those VAR bits
   if (var == 512) e = launch_attn_long_pp<0>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 640) e = launch_attn_long_pp<128>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);

@@ -2,6 +2,8 @@
 // product library (attention_long.hip: VAR = 0) and the tools' diag library (tools/diag/csrc:
 // variants for A/B).  Design notes: attention_long.hip.
 #pragma once
+#include <type_traits>
+
 #include "vp_common.h"
 #include "vp_kernels.h"
 
@@ -20,6 +22,40 @@ __device__ __forceinline__ float capped_exp(float x, float two_log2e_over_cap, f
 __device__ __forceinline__ int swzK(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swzV(int row) { return ((row >> 1) & 1) << 2; }
 
+// the K / V reads of lds_read4_b128 / lds_tr_read8 (vp_common.h) from per-lane base addresses plus a compile-time
+// offset (the chunk loop unrolled over the 4 stages, so a tile's stage and key offsets are immediates and the
+// per-tile address arithmetic disappears); same form (i): reads and their wait in one statement
+template <int OFF>
+__device__ __forceinline__ void lds_read4_b128_o(bf16x8 (&v)[4], const uint32_t (&ad)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4 offset:%8\n\t"
+      "ds_read_b128 %1, %5 offset:%8\n\t"
+      "ds_read_b128 %2, %6 offset:%8\n\t"
+      "ds_read_b128 %3, %7 offset:%8\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "n"(OFF)
+      : "memory");
+}
+// v[s][dh][hf] <- ad[dh] + OFF + 2048 s + 1024 hf
+template <int OFF>
+__device__ __forceinline__ void lds_tr_read8_o(s16x4 (&v)[2][2][2], const uint32_t (&ad)[2]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8 offset:%10\n\t"
+      "ds_read_b64_tr_b16 %1, %8 offset:%11\n\t"
+      "ds_read_b64_tr_b16 %2, %9 offset:%10\n\t"
+      "ds_read_b64_tr_b16 %3, %9 offset:%11\n\t"
+      "ds_read_b64_tr_b16 %4, %8 offset:%12\n\t"
+      "ds_read_b64_tr_b16 %5, %8 offset:%13\n\t"
+      "ds_read_b64_tr_b16 %6, %9 offset:%12\n\t"
+      "ds_read_b64_tr_b16 %7, %9 offset:%13\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0][0][0]), "=&v"(v[0][0][1]), "=&v"(v[0][1][0]), "=&v"(v[0][1][1]), "=&v"(v[1][0][0]),
+        "=&v"(v[1][0][1]), "=&v"(v[1][1][0]), "=&v"(v[1][1][1])
+      : "v"(ad[0]), "v"(ad[1]), "n"(OFF), "n"(OFF + 1024), "n"(OFF + 2048), "n"(OFF + 3072)
+      : "memory");
+}
+
 constexpr int kLgThreads = 512;          // 8 waves x 32 queries
 constexpr int kLgQ = 256;                // queries per workgroup
 constexpr int kLgChunk = 64;             // keys per LDS stage
@@ -36,7 +72,10 @@ constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 // one value at a time; 8 = no linear tier; 16 = the row sum on the MFMA (a ones A operand against the
 // bf16 numerators, so the sum of the rounded values P.V uses); 32 = the row sum by v_dot2_f32_bf16 of
 // the bf16 numerator pairs; 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32; 128 = the LIN
-// tier in packed pairs; 256 = s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4).
+// tier in packed pairs; 256 = s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4); 1024 =
+// round 5's chunk loop with the stage and the K / V read addresses computed per tile (the product unrolls the chunk
+// loop over the 4 LDS stages, so the reads take per-lane bases + immediate offsets: bitwise the same, 2.4-3.7 %
+// faster at logit std 0.5 / 2 / 6, profiles/r06/aux_attention_stage_unroll.txt).
 // TAIL: S % 256 != 0 (S > 256; frame sizes whose T*N is not a multiple of 256, encoders.py:846-857 takes any
 // T*N): nqb = ceil(S / 256) and ceil(S / 64) chunks; a query or key row past S is read from row S - 1 (so
 // every load stays inside the sequence), the numerators of keys past S are zeroed before the row sum and
@@ -111,8 +150,22 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
     if (w >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
   }
 
-#pragma unroll 1
-  for (int c = 0; c < nchunks; ++c) {
+  // per-lane K / V read bases of the stage-unrolled loop (stage and key offsets are immediates there): krow = kt 32 + krow_l, so
+  // swzK(krow) = (krow_l >> 1) & 7 and, for key = kt 32 + 16 s + 4 half + trq, swzV(key) = ((trq >> 1) & 1) << 2
+  [[maybe_unused]] uint32_t kb[4], vb[2];
+  if constexpr ((VAR & 1024) == 0) {
+    const uint32_t sb = (uint32_t)(uintptr_t)VP_LDS_PTR(smem);
+#pragma unroll
+    for (int kd = 0; kd < 4; ++kd) kb[kd] = sb + krow_l * 128 + (((2 * kd + half) ^ ((krow_l >> 1) & 7)) << 4);
+#pragma unroll
+    for (int dh = 0; dh < 2; ++dh) {
+      const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
+      vb[dh] = sb + (4 * half + trq) * 128 + (((col >> 3) ^ (((trq >> 1) & 1) << 2)) << 4) + (col & 7) * 2;
+    }
+  }
+  // one 64-key chunk: STG = its LDS stage as a compile-time constant (the product), or -1 (c % 4 at run time, VAR 1024)
+  auto chunk = [&](int c, auto STG) {
+    constexpr int stg = decltype(STG)::value;
     // this wave's pieces of chunk c have landed when at most the younger chunks' pieces
     // (2 per chunk) are outstanding; then one barrier makes every wave's pieces visible and
     // retires all reads of stage (c - 1) % 4, which chunk c + 3 overwrites
@@ -125,21 +178,25 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
     __builtin_amdgcn_sched_barrier(0);
     if (c + kLgStages - 1 < nchunks) issue(c + kLgStages - 1);
     const char* Ks = smem + (c & (kLgStages - 1)) * kLgStageBytes;
-    const char* Vs = Ks + kLgChunk * 128;
-#pragma unroll
-    for (int kt = 0; kt < kLgChunk / 32; ++kt) {
+    [[maybe_unused]] const char* Vs = Ks + kLgChunk * 128;
+    auto tile = [&](auto KT) {
+      constexpr int kt = decltype(KT)::value;
       f32x16 x = {};
       const int krow = kt * 32 + krow_l;
       // K and V reads: inline asm (a visible LDS read would get a vmcnt(0) for the chunks still
       // landing), reads and wait in one statement (vp_common.h lds_read4_b128 / lds_tr_read8)
       bf16x8 kf[4];
-      uint32_t kad[4];
+      if constexpr (stg >= 0) {
+        lds_read4_b128_o<stg * kLgStageBytes + kt * 4096>(kf, kb);
+      } else {
+        uint32_t kad[4];
 #pragma unroll
-      for (int kd = 0; kd < 4; ++kd) {
-        const int cc = 2 * kd + half;
-        kad[kd] = (uint32_t)(uintptr_t)VP_LDS_PTR(Ks + krow * 128 + ((cc ^ swzK(krow)) << 4));
+        for (int kd = 0; kd < 4; ++kd) {
+          const int cc = 2 * kd + half;
+          kad[kd] = (uint32_t)(uintptr_t)VP_LDS_PTR(Ks + krow * 128 + ((cc ^ swzK(krow)) << 4));
+        }
+        lds_read4_b128(kf, kad);
       }
-      lds_read4_b128(kf, kad);
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
       float p[16];
@@ -189,19 +246,23 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
         ysum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[0], ysum, 0, 0, 0);
         ysum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[1], ysum, 0, 0, 0);
       }
-      uint32_t vad[2][2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int key = kt * 32 + 16 * s + 4 * half + trq;
-#pragma unroll
-        for (int dh = 0; dh < 2; ++dh) {
-          const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
-          const int cc = col >> 3;
-          vad[s][dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((cc ^ swzV(key)) << 4) + (col & 7) * 2);
-        }
-      }
       s16x4 vr[2][2][2];
-      lds_tr_read8(vr, vad);
+      if constexpr (stg >= 0) {
+        lds_tr_read8_o<stg * kLgStageBytes + kLgChunk * 128 + kt * 4096>(vr, vb);
+      } else {
+        uint32_t vad[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int key = kt * 32 + 16 * s + 4 * half + trq;
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) {
+            const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
+            const int cc = col >> 3;
+            vad[s][dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((cc ^ swzV(key)) << 4) + (col & 7) * 2);
+          }
+        }
+        lds_tr_read8(vr, vad);
+      }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -213,7 +274,21 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
           else y1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[s], y1, 0, 0, 0);
         }
       }
+    };
+    tile(std::integral_constant<int, 0>{});
+    tile(std::integral_constant<int, 1>{});
+  };
+  if constexpr ((VAR & 1024) == 0) {
+#pragma unroll 1
+    for (int c0 = 0; c0 < nchunks; c0 += kLgStages) {
+      chunk(c0, std::integral_constant<int, 0>{});
+      if (c0 + 1 < nchunks) chunk(c0 + 1, std::integral_constant<int, 1>{});
+      if (c0 + 2 < nchunks) chunk(c0 + 2, std::integral_constant<int, 2>{});
+      if (c0 + 3 < nchunks) chunk(c0 + 3, std::integral_constant<int, 3>{});
     }
+  } else {
+#pragma unroll 1
+    for (int c = 0; c < nchunks; ++c) chunk(c, std::integral_constant<int, -1>{});
   }
   if constexpr ((VAR & 16) != 0) {
     lsum = ysum[0];  // every row of the ones product holds the full sum of its query column
