@@ -73,7 +73,7 @@ def test_asm_loads_waited_or_audited(audited_asm):
     assert form2 == {"attention", "attention_long_kernel"}
     # the LDS reads of both attention kernels are form (i): reads + wait in one statement
     common = ck.asm_loads(open(os.path.join(CSRC, "vp_common.h")).read())
-    assert len(common) == 2 and all(f == "i" for _, f in common)
+    assert len(common) == 4 and all(f == "i" for _, f in common)  # base-address and immediate-offset forms
 
 
 def _inject_after_first_asm_load(src_path, dst_path, make_line):

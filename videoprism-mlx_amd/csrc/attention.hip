@@ -164,8 +164,19 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     }
     return x;
   };
+  // per-lane V read bases (lds_tr_read8_o): for key = kt 32 + 16 s + 4 half + trq, swzV(key) = ((trq >> 1) & 1) << 2,
+  // so a tile's V addresses are these plus the immediate kt 4096 (+ 2048 s, + 1024 for the upper 4 rows)
+  [[maybe_unused]] uint32_t vb[2];
+#pragma unroll
+  for (int dh = 0; dh < 2; ++dh) {
+    const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
+    vb[dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + (4 * half + trq) * 128 + (((col >> 3) ^ (((trq >> 1) & 1) << 2)) << 4) +
+                                             (col & 7) * 2);
+  }
   // numerators of tile kt, then O^T += V^T . X
-  auto pv = [&](int kt, const f32x16& x) {
+  // OFFT: the tile's V offset kt * 4096 as a compile-time constant (the unrolled unmasked form), or -1 (run time)
+  auto pv = [&](int kt, auto OFFT, const f32x16& x) {
+    constexpr int voff = decltype(OFFT)::value;
     // numerators: register i <-> key kt*32 + (i&3) + 8(i>>2) + 4*half (exact three-transcendental
     // form: the one-transcendental polynomial moved the full-depth LvT-B bf16 embedding across the
     // 1e-3 bar)
@@ -196,19 +207,23 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     // lgkmcnt(0) in ONE statement with early-clobber outputs: the destinations are defined only
     // once the data has landed, so no compiler copy or spill can touch them in flight
     // (cdna_hip_programming.md §5.7 item 1, form (i))
-    uint32_t ad[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int key = kt * 32 + 16 * s + 4 * half + trq;
-#pragma unroll
-      for (int dh = 0; dh < 2; ++dh) {
-        const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
-        const int c = col >> 3;
-        ad[s][dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2);
-      }
-    }
     s16x4 vr[2][2][2];
-    lds_tr_read8(vr, ad);
+    if constexpr (voff >= 0) {
+      lds_tr_read8_o<voff>(vr, vb);
+    } else {
+      uint32_t ad[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int key = kt * 32 + 16 * s + 4 * half + trq;
+#pragma unroll
+        for (int dh = 0; dh < 2; ++dh) {
+          const int col = 32 * dh + 16 * (g & 1) + 4 * trp;
+          const int c = col >> 3;
+          ad[s][dh] = (uint32_t)(uintptr_t)VP_LDS_PTR(Vs + key * 128 + ((c ^ swzV(key)) << 4) + (col & 7) * 2);
+        }
+      }
+      lds_tr_read8(vr, ad);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -222,17 +237,31 @@ __global__ __launch_bounds__(kSpThreads, 4) void attn_spatial_kernel(
     }
   };
 
-  chunk_ready(std::integral_constant<int, 0>{});
   // (a software-pipelined form -- the S^T MFMAs of tile kt+1 issued ahead of tile kt's
   // numerators -- is bitwise equal but measured 289.8 vs 206.8 us: at 128 VGPRs it spills inside
-  // the loop; profiles/HISTORY.md round 3)
+  // the loop; profiles/HISTORY.md round 3.)  Unmasked (round 6): the 8 tiles written out, so every K / V read address
+  // is a per-lane base plus an immediate offset (no per-tile address arithmetic); the masked form keeps the loop (its
+  // key-padding reads would spill written out)
+  chunk_ready(std::integral_constant<int, 0>{});
+  if constexpr (!MASK) {
+    using std::integral_constant;
+    pv(0, integral_constant<int, 0 * 4096>{}, qk(0));
+    pv(1, integral_constant<int, 1 * 4096>{}, qk(1));
+    chunk_ready(integral_constant<int, 1>{});
+    pv(2, integral_constant<int, 2 * 4096>{}, qk(2));
+    pv(3, integral_constant<int, 3 * 4096>{}, qk(3));
+    chunk_ready(integral_constant<int, 2>{});
+    pv(4, integral_constant<int, 4 * 4096>{}, qk(4));
+    pv(5, integral_constant<int, 5 * 4096>{}, qk(5));
+    chunk_ready(integral_constant<int, 3>{});
+    pv(6, integral_constant<int, 6 * 4096>{}, qk(6));
+    pv(7, integral_constant<int, 7 * 4096>{}, qk(7));
+  } else {
 #pragma unroll 1
-  for (int cc = 0; cc < 4; ++cc) {
-    if (cc == 1) chunk_ready(std::integral_constant<int, 1>{});
-    else if (cc == 2) chunk_ready(std::integral_constant<int, 2>{});
-    else if (cc == 3) chunk_ready(std::integral_constant<int, 3>{});
+    for (int cc = 0; cc < 4; ++cc) {
 #pragma unroll 2
-    for (int kt = 2 * cc; kt < 2 * cc + 2; ++kt) pv(kt, qk(kt));
+      for (int kt = 2 * cc; kt < 2 * cc + 2; ++kt) pv(kt, std::integral_constant<int, -1>{}, qk(kt));
+    }
   }
   lsum += __shfl_xor(lsum, 32);
   const float inv = 1.0f / lsum;

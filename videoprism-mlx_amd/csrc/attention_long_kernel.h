@@ -22,40 +22,6 @@ __device__ __forceinline__ float capped_exp(float x, float two_log2e_over_cap, f
 __device__ __forceinline__ int swzK(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swzV(int row) { return ((row >> 1) & 1) << 2; }
 
-// the K / V reads of lds_read4_b128 / lds_tr_read8 (vp_common.h) from per-lane base addresses plus a compile-time
-// offset (the chunk loop unrolled over the 4 stages, so a tile's stage and key offsets are immediates and the
-// per-tile address arithmetic disappears); same form (i): reads and their wait in one statement
-template <int OFF>
-__device__ __forceinline__ void lds_read4_b128_o(bf16x8 (&v)[4], const uint32_t (&ad)[4]) {
-  asm volatile(
-      "ds_read_b128 %0, %4 offset:%8\n\t"
-      "ds_read_b128 %1, %5 offset:%8\n\t"
-      "ds_read_b128 %2, %6 offset:%8\n\t"
-      "ds_read_b128 %3, %7 offset:%8\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
-      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "n"(OFF)
-      : "memory");
-}
-// v[s][dh][hf] <- ad[dh] + OFF + 2048 s + 1024 hf
-template <int OFF>
-__device__ __forceinline__ void lds_tr_read8_o(s16x4 (&v)[2][2][2], const uint32_t (&ad)[2]) {
-  asm volatile(
-      "ds_read_b64_tr_b16 %0, %8 offset:%10\n\t"
-      "ds_read_b64_tr_b16 %1, %8 offset:%11\n\t"
-      "ds_read_b64_tr_b16 %2, %9 offset:%10\n\t"
-      "ds_read_b64_tr_b16 %3, %9 offset:%11\n\t"
-      "ds_read_b64_tr_b16 %4, %8 offset:%12\n\t"
-      "ds_read_b64_tr_b16 %5, %8 offset:%13\n\t"
-      "ds_read_b64_tr_b16 %6, %9 offset:%12\n\t"
-      "ds_read_b64_tr_b16 %7, %9 offset:%13\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(v[0][0][0]), "=&v"(v[0][0][1]), "=&v"(v[0][1][0]), "=&v"(v[0][1][1]), "=&v"(v[1][0][0]),
-        "=&v"(v[1][0][1]), "=&v"(v[1][1][0]), "=&v"(v[1][1][1])
-      : "v"(ad[0]), "v"(ad[1]), "n"(OFF), "n"(OFF + 1024), "n"(OFF + 2048), "n"(OFF + 3072)
-      : "memory");
-}
-
 constexpr int kLgThreads = 512;          // 8 waves x 32 queries
 constexpr int kLgQ = 256;                // queries per workgroup
 constexpr int kLgChunk = 64;             // keys per LDS stage
