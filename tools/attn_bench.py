@@ -58,8 +58,7 @@ def long_variants():
     """The auxiliary (4096-token) attention at the LvT-Large bench shape (32 clips x 16 heads, S = 4096):
     the product kernel (var 0) against its diag-library A/B builds (attention_long_kernel.h VAR bits:
     8: without the linear tier for |logit| <= 0.10 cap = round 4's kernel; 16: row sum on the MFMA;
-    32: row sum by v_dot2_f32_bf16; 64: unpaired scalar numerator and row sum; 80, 96 combined; 2048: logits
-    pre-scaled by cap_beta, q scaled by beta before its bf16 rounding, so compared by value; 4096: no tier check), at three
+    32: row sum by v_dot2_f32_bf16; 64: unpaired scalar numerator and row sum; 80, 96 combined), at three
     logit scales (std 0.5 / 2 / 6: linear, quadratic / cubic and mixed tiers), interleaved rounds.
     VP_DIAG_LIB=1 python tools/attn_bench.py long   (VP_ATTN_VARIANTS=0,8 picks the builds)"""
     dev = torch.device("cuda:0")
@@ -71,17 +70,12 @@ def long_variants():
         g = torch.Generator(device=dev).manual_seed(0)
         qkv = torch.randn((nseq * S, 3 * D), generator=g, device=dev)
         qkv[:, :D] *= qscale
-        # VAR bit 2048 takes logits pre-scaled by cap_beta: q scaled before its one bf16 rounding
-        beta = nat.load().vp_dev_cap_beta(50.0)
-        qkvb = qkv.clone()
-        qkvb[:, :D] *= beta
-        qkv, qkvb = qkv.to(torch.bfloat16), qkvb.to(torch.bfloat16)
+        qkv = qkv.to(torch.bfloat16)
         outs, fns = {}, {}
         for var in variants:
             outs[var] = torch.empty((nseq * S, D), device=dev, dtype=torch.bfloat16)
-            src = qkvb if var & 2048 else qkv
-            fns[f"var{var}"] = (lambda var=var, src=src: nat.call("vp_dev_attention_long_var", var, src.data_ptr(),
-                                                                  outs[var].data_ptr(), nseq, S, heads, 50.0, st()))
+            fns[f"var{var}"] = (lambda var=var: nat.call("vp_dev_attention_long_var", var, qkv.data_ptr(),
+                                                         outs[var].data_ptr(), nseq, S, heads, 50.0, st()))
         for f in fns.values():
             f()
         torch.cuda.synchronize()
@@ -96,7 +90,7 @@ def long_variants():
         flop = 4.0 * nseq * S * S * D
         print("aux attention:", " ".join(f"{k}: {min(v):7.3f} ms ({flop/min(v)/1e9:5.0f} TF)" for k, v in res.items()),
               flush=True)
-        del qkv, qkvb, outs
+        del qkv, outs
 
 
 if __name__ == "__main__":

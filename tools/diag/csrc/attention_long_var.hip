@@ -5,12 +5,9 @@
 // (round 4's product kernel), 16 = the row sum on the MFMA, 32 = the row sum by v_dot2_f32_bf16,
 // 64 = the LIN / QUAD tiers and the row sum in unpaired scalar fp32, 128 = the LIN tier packed, 256 = s_setprio 1
 // for waves 4-7, 1024 = round 5's chunk loop (addresses per tile; the product unrolls over the LDS stages)
-// (bits combine: 6 = round 3's kernel); 2048 = logits pre-scaled by cap_beta (the caller scales q), 4096 = no tier
-// check (timing only), 8192 = V reads with the K reads, 16384 = V reads before the numerators.
+// (bits combine: 6 = round 3's kernel).
 #include "attention_long_kernel.h"
 #include "attention_long_pp.h"
-
-extern "C" double vp_dev_cap_beta(float cap) { return vp::cap_beta(cap); }
 
 extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int64_t num_seq, int64_t S,
                                          int64_t heads, float cap, void* stream) {
@@ -36,16 +33,6 @@ extern "C" int vp_dev_attention_long_var(int var, const void* qkv, void* o, int6
   if (var == 512) e = launch_attn_long_pp<0>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 640) e = launch_attn_long_pp<128>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 768) e = launch_attn_long_pp<256>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 2048) e = launch_attn_long<2048>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 4096) e = launch_attn_long<4096>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 6144) e = launch_attn_long<6144>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 8192) e = launch_attn_long<8192>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 16384) e = launch_attn_long<16384>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 10240) e = launch_attn_long<10240>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 18432) e = launch_attn_long<18432>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 32768) e = launch_attn_long<32768>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 65536) e = launch_attn_long<65536>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
-  if (var == 98304) e = launch_attn_long<98304>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   if (var == 7) e = launch_attn_long<7>((const bf16_t*)qkv, (bf16_t*)o, (int)num_seq, (int)S, (int)heads, cap, s);
   return e == hipSuccess ? 0 : -1;
 }

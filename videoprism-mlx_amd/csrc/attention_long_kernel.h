@@ -41,11 +41,7 @@ constexpr int kLgLds = kLgStages * kLgStageBytes;  // 64 KiB
 // tier in packed pairs; 256 = s_setprio 1 for waves 4-7 (MI355X_MICROARCH.md, two waves per SIMD, item 4); 1024 =
 // round 5's chunk loop with the stage and the K / V read addresses computed per tile (the product unrolls the chunk
 // loop over the 4 LDS stages, so the reads take per-lane bases + immediate offsets: bitwise the same, 2.4-3.7 %
-// faster at logit std 0.5 / 2 / 6, profiles/r06/aux_attention_stage_unroll.txt); 2048 = logits pre-scaled by
-// cap_beta(cap) (q scaled by the caller), the LIN tier in two operations; 4096 = no tier check, LIN for every tile
-// (timing only: exact only when every logit is in the LIN range); 8192 = a tile's V reads issued with its K reads (one
-// LDS wait per tile); 16384 = the V reads issued after the S^T MFMAs, before the numerators; 32768 / 65536 = no V / no K
-// LDS reads (timing only).
+// faster at logit std 0.5 / 2 / 6, profiles/r06/aux_attention_stage_unroll.txt).
 // TAIL: S % 256 != 0 (S > 256; frame sizes whose T*N is not a multiple of 256, encoders.py:846-857 takes any
 // T*N): nqb = ceil(S / 256) and ceil(S / 64) chunks; a query or key row past S is read from row S - 1 (so
 // every load stays inside the sequence), the numerators of keys past S are zeroed before the row sum and
@@ -105,7 +101,7 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
   // chunk-0 wait is then a no-op
   asm volatile("s_waitcnt vmcnt(4)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]) : : "memory");
 
-  const float c1 = (VAR & 2048) != 0 ? cp.e1 : 2.0f * kLog2e / cap;
+  const float c1 = 2.0f * kLog2e / cap;
   const float c2 = cap * kLog2e;
   f32x16 y0 = {}, y1 = {};
   [[maybe_unused]] f32x16 ysum = {};
@@ -156,16 +152,7 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
       // K and V reads: inline asm (a visible LDS read would get a vmcnt(0) for the chunks still
       // landing), reads and wait in one statement (vp_common.h lds_read4_b128 / lds_tr_read8)
       bf16x8 kf[4];
-      // VAR 8192: the tile's V reads issued with its K reads (one wait); VAR 16384: after the S^T MFMAs, before the
-      // numerators (stage-unrolled loop only)
-      constexpr bool kv_early = (VAR & 8192) != 0 && stg >= 0, v_mid = (VAR & 16384) != 0 && stg >= 0;
-      s16x4 vr[2][2][2];
-      if constexpr (kv_early) {
-        lds_read_kv_o<stg * kLgStageBytes + kt * 4096, stg * kLgStageBytes + kLgChunk * 128 + kt * 4096>(kf, kb, vr, vb);
-      } else if constexpr ((VAR & 65536) != 0) {  // timing only: no K reads (K fragments = Q fragments)
-#pragma unroll
-        for (int kd = 0; kd < 4; ++kd) kf[kd] = qf[kd];
-      } else if constexpr (stg >= 0) {
+      if constexpr (stg >= 0) {
         lds_read4_b128_o<stg * kLgStageBytes + kt * 4096>(kf, kb);
       } else {
         uint32_t kad[4];
@@ -178,10 +165,9 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
       }
 #pragma unroll
       for (int kd = 0; kd < 4; ++kd) x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kd], qf[kd], x, 0, 0, 0);
-      if constexpr (v_mid) lds_tr_read8_o<stg * kLgStageBytes + kLgChunk * 128 + kt * 4096>(vr, vb);
       float p[16];
-      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0, (VAR & 64) != 0, (VAR & 128) != 0,
-                   (VAR & 2048) != 0, (VAR & 4096) != 0>(x, p, c1, c2, cp);
+      capped_exp16<(VAR & 1) == 0, (VAR & 2) == 0, (VAR & 8) == 0, (VAR & 64) != 0, (VAR & 128) != 0>(x, p, c1, c2,
+                                                                                                     cp);
       if constexpr (TAIL) {
         // keys past S (the last chunk only): weight 0.  Lane l, value i holds key row
         // 8 (i / 4) + 4 (l / 32) + i % 4 of the 32-key tile (the 32x32 MFMA output layout)
@@ -226,17 +212,8 @@ __global__ __launch_bounds__(kLgThreads, 4) void attn_long_kernel(const bf16_t* 
         ysum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[0], ysum, 0, 0, 0);
         ysum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[1], ysum, 0, 0, 0);
       }
-      if constexpr (kv_early || v_mid) {
-      } else if constexpr ((VAR & 32768) != 0) {  // timing only: no V reads (V fragments from the Q fragments)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh)
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf)
-              vr[s][dh][hf] = s16x4{qf[2 * s + dh][4 * hf], qf[2 * s + dh][4 * hf + 1], qf[2 * s + dh][4 * hf + 2],
-                                    qf[2 * s + dh][4 * hf + 3]};
-      } else if constexpr (stg >= 0) {
+      s16x4 vr[2][2][2];
+      if constexpr (stg >= 0) {
         lds_tr_read8_o<stg * kLgStageBytes + kLgChunk * 128 + kt * 4096>(vr, vb);
       } else {
         uint32_t vad[2][2];
@@ -308,7 +285,7 @@ hipError_t launch_attn_long_t(const bf16_t* qkv, bf16_t* o, int num_seq, int S, 
   const int64_t grid = (int64_t)num_seq * heads * nqb;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   const int xcd_map = grid % 8 == 0 ? 1 : 0;
-  const CapPoly cp = make_cap_poly(cap, (VAR & 2048) != 0);
+  const CapPoly cp = make_cap_poly(cap);
   VP_NOTE_KERNEL(fn);
   hipLaunchKernelGGL((attn_long_kernel<VAR, TAIL>), dim3((unsigned)grid), dim3(kLgThreads), kLgLds, s, qkv, o, S,
                      heads, nqb, cap, xcd_map, cp);

@@ -4,7 +4,6 @@
 #include <stdint.h>
 
 #include <atomic>
-#include <cmath>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -84,36 +83,17 @@ struct CapPoly {
   float k0, k1, k2, k3, x0;
   float q0, q1, q2, x1;
   float l0, l1, x2;
-  float lk, e1;  // logits pre-scaled by beta (make_cap_poly(cap, true)): LIN = x (x^2 + lk); exact tier exp2(x e1)
 };
 
-constexpr double kCapLinW0 = 0.9999983358095185, kCapLinW1 = -0.33200482774291656;
-
-// the logit scale beta with beta^3 = log2e w1 / cap^2 (the LIN tier's cubic coefficient): logits computed as
-// beta * x make the LIN exponent x' (x'^2 + lk) -- two VALU operations per logit instead of three
-inline double cap_beta(float cap) {
-  return std::cbrt(1.4426950408889634 * kCapLinW1 / ((double)cap * cap));
-}
-
-// BETA: the coefficients for logits pre-scaled by cap_beta(cap) (every tier: powers of 1 / beta folded in,
-// thresholds scaled by |beta|); otherwise for the logits themselves
-inline CapPoly make_cap_poly(float cap, bool BETA = false) {
+inline CapPoly make_cap_poly(float cap) {
   const double t[4] = {0.9999995827674866, -0.33327752351760864, 0.1321016252040863, -0.045063190162181854};
   const double u[3] = {0.9999996877028773, -0.33323595618512314, 0.12879159575308177};
-  const double w[2] = {kCapLinW0, kCapLinW1};
+  const double w[2] = {0.9999983358095185, -0.33200482774291656};
   const double l2e = 1.4426950408889634, c2 = (double)cap * cap;
-  if (!BETA)
-    return CapPoly{(float)(l2e * t[0]), (float)(l2e * t[1] / c2), (float)(l2e * t[2] / (c2 * c2)),
-                   (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap,
-                   (float)(l2e * u[0]), (float)(l2e * u[1] / c2), (float)(l2e * u[2] / (c2 * c2)), 0.24f * cap,
-                   (float)(l2e * w[0]), (float)(l2e * w[1] / c2), 0.10f * cap, 0.0f, 2.0f * 1.4426950408889634f / cap};
-  const double b = cap_beta(cap), b2 = b * b, ab = std::fabs(b);
-  return CapPoly{(float)(l2e * t[0] / b), (float)(l2e * t[1] / (c2 * b * b2)), (float)(l2e * t[2] / (c2 * c2 * b * b2 * b2)),
-                 (float)(l2e * t[3] / (c2 * c2 * c2 * b * b2 * b2 * b2)), (float)(0.48 * cap * ab),
-                 (float)(l2e * u[0] / b), (float)(l2e * u[1] / (c2 * b * b2)), (float)(l2e * u[2] / (c2 * c2 * b * b2 * b2)),
-                 (float)(0.24 * cap * ab),
-                 (float)(l2e * w[0] / b), (float)(l2e * w[1] / (c2 * b * b2)), (float)(0.10 * cap * ab),
-                 (float)(l2e * w[0] / b), (float)(2.0 * l2e / (cap * b))};
+  return CapPoly{(float)(l2e * t[0]), (float)(l2e * t[1] / c2), (float)(l2e * t[2] / (c2 * c2)),
+                 (float)(l2e * t[3] / (c2 * c2 * c2)), 0.48f * cap,
+                 (float)(l2e * u[0]), (float)(l2e * u[1] / c2), (float)(l2e * u[2] / (c2 * c2)), 0.24f * cap,
+                 (float)(l2e * w[0]), (float)(l2e * w[1] / c2), 0.10f * cap};
 }
 
 // PACKED: the polynomial in pairs of packed fp32 (v_pk_mul_f32 / v_pk_fma_f32), else scalar fp32
@@ -133,19 +113,13 @@ __device__ __forceinline__ float fma_s(float a, float b, float c) {
 
 // SCALAR (A/B builds): the LIN / QUAD tiers in unpaired scalar fp32 (the same IEEE operations); PKLIN (A/B
 // builds): the LIN tier in packed pairs (the same IEEE operations, half the instructions)
-template <bool PACKED = true, bool QUAD = false, bool LIN = false, bool SCALAR = false, bool PKLIN = false,
-          bool BETA = false, bool NOCHK = false>
+template <bool PACKED = true, bool QUAD = false, bool LIN = false, bool SCALAR = false, bool PKLIN = false>
 __device__ __forceinline__ void capped_exp16(const f32x16& x, float* p, float c1, float c2, const CapPoly& cp) {
   float mx = 0.0f;
-  if constexpr (!NOCHK) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
-  }
-  if (LIN && (NOCHK || __builtin_amdgcn_ballot_w64(mx > cp.x2) == 0)) {
-    if constexpr (BETA) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) p[i] = __builtin_amdgcn_exp2f(x[i] * fmaf(x[i], x[i], cp.lk));
-    } else if constexpr (PKLIN) {
+  for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
+  if (LIN && __builtin_amdgcn_ballot_w64(mx > cp.x2) == 0) {
+    if constexpr (PKLIN) {
       typedef float f2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
@@ -298,32 +272,6 @@ __device__ __forceinline__ void lds_tr_read8_o(s16x4 (&v)[2][2][2], const uint32
       : "=&v"(v[0][0][0]), "=&v"(v[0][0][1]), "=&v"(v[0][1][0]), "=&v"(v[0][1][1]), "=&v"(v[1][0][0]),
         "=&v"(v[1][0][1]), "=&v"(v[1][1][0]), "=&v"(v[1][1][1])
       : "v"(ad[0]), "v"(ad[1]), "n"(OFF), "n"(OFF + 1024), "n"(OFF + 2048), "n"(OFF + 3072)
-      : "memory");
-}
-
-// the K reads of lds_read4_b128_o<KOFF> and the V reads of lds_tr_read8_o<VOFF> in one statement (one wait)
-template <int KOFF, int VOFF>
-__device__ __forceinline__ void lds_read_kv_o(bf16x8 (&k)[4], const uint32_t (&ka)[4], s16x4 (&v)[2][2][2],
-                                              const uint32_t (&va)[2]) {
-  asm volatile(
-      "ds_read_b128 %0, %12 offset:%18\n\t"
-      "ds_read_b128 %1, %13 offset:%18\n\t"
-      "ds_read_b128 %2, %14 offset:%18\n\t"
-      "ds_read_b128 %3, %15 offset:%18\n\t"
-      "ds_read_b64_tr_b16 %4, %16 offset:%19\n\t"
-      "ds_read_b64_tr_b16 %5, %16 offset:%20\n\t"
-      "ds_read_b64_tr_b16 %6, %17 offset:%19\n\t"
-      "ds_read_b64_tr_b16 %7, %17 offset:%20\n\t"
-      "ds_read_b64_tr_b16 %8, %16 offset:%21\n\t"
-      "ds_read_b64_tr_b16 %9, %16 offset:%22\n\t"
-      "ds_read_b64_tr_b16 %10, %17 offset:%21\n\t"
-      "ds_read_b64_tr_b16 %11, %17 offset:%22\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(k[0]), "=&v"(k[1]), "=&v"(k[2]), "=&v"(k[3]), "=&v"(v[0][0][0]), "=&v"(v[0][0][1]),
-        "=&v"(v[0][1][0]), "=&v"(v[0][1][1]), "=&v"(v[1][0][0]), "=&v"(v[1][0][1]), "=&v"(v[1][1][0]),
-        "=&v"(v[1][1][1])
-      : "v"(ka[0]), "v"(ka[1]), "v"(ka[2]), "v"(ka[3]), "v"(va[0]), "v"(va[1]), "n"(KOFF), "n"(VOFF),
-        "n"(VOFF + 1024), "n"(VOFF + 2048), "n"(VOFF + 3072)
       : "memory");
 }
 

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_void_p
 
 _LIB_NAME = "libvideoprism_hip.so"
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
@@ -149,7 +149,6 @@ _SIGNATURES = {
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
     "vp_dev_attention_long_var": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p]),
-    "vp_dev_cap_beta": (c_double, [c_float]),
     "vp_dev_gemm_tattn_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_w4_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
