@@ -2,7 +2,7 @@
 the max-free softmax's range (layers.py:586-589: cap <= 0 disables capping; FactorizedEncoder's
 default cap is 0.0, encoders.py:407), the host engine's argument validation, the per-class kernel
 symbol the bench's roofline keys its PMC record on, and the C-ABI RCCL all-gather (vp_allgather)
-on a one-rank communicator."""
+on a one-rank communicator, and empty batches (zero-size results, as the reference's JAX graph)."""
 
 import os
 
@@ -185,3 +185,46 @@ def test_bench_base_step_world1_gather_vs_fixture(cuda):
         assert err <= 1e-3
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_empty_batch_zero_size_results(cuda, bf16):
+    """B = 0 clips (and Q = 0 text queries): the reference's JAX graph maps zero-size arrays to
+    zero-size results (encoders.py:436 reshapes [0, T, H, W, 3] to [0, H, W, 3]; every later op is
+    shape-polymorphic), so the drop-in returns [0, T*N, D] embeddings (and zero-size intermediates,
+    logits, video / text embeddings) instead of an error; the geometry and frame_paddings checks still
+    apply, and a following non-empty forward is unaffected."""
+    dt = torch.bfloat16 if bf16 else None
+    cfg = _cfg()
+    var = params.synthetic_params(cfg, seed=3)
+    mdl = _model(cfg, bf16)
+    emb, out = mdl.apply(var, np.zeros((0, 2, 288, 288, 3), np.float32), return_intermediate=True,
+                         frame_paddings=np.zeros((0, 2), np.float32))
+    assert emb.shape == (0, 512, 768) and out["spatial_features"].shape == (0, 512, 768)
+    with pytest.raises(ValueError):
+        mdl.apply(var, np.zeros((0, 2, 280, 280, 3), np.float32))  # 280 % 18 != 0, as the reference
+    with pytest.raises(AssertionError):
+        mdl.apply(var, np.zeros((0, 2, 288, 288, 3), np.float32), frame_paddings=np.zeros((1, 2), np.float32))
+    video = np.random.default_rng(3).random((1, 2, 288, 288, 3), dtype=np.float32)
+    e1, _ = mdl.apply(var, video)
+    ref, _ = orc.factorized_encoder(var["params"], video, cfg, mode="f64")
+    assert np.abs(_pool_l2(e1) - _pool_l2(ref)).max() <= (1e-3 if bf16 else 1e-5)
+
+    ccfg = dict(models.CONFIGS["videoprism_lvt_v1_base"])
+    ccfg.update(num_spatial_layers=1, num_temporal_layers=1, num_auxiliary_layers=1, num_unimodal_layers=1,
+                vocabulary_size=100)
+    clip = models.get_model(None, model_fn=lambda: models.encoders.FactorizedVideoCLIP(**ccfg), fprop_dtype=dt)
+    cvar = params.synthetic_params(ccfg, seed=3, specs=params.clip_leaf_specs(ccfg))
+    v, t, cout = clip.apply(cvar, np.zeros((0, 2, 288, 288, 3), np.float32), np.zeros((0, 16), np.int32),
+                            np.zeros((0, 16), np.float32), return_intermediate=True)
+    assert v.shape == (0, 768) and t.shape == (0, 768)
+    assert cout["frame_embeddings"].shape == (0, 2, 768) and cout["spatiotemporal_features"].shape == (0, 512, 768)
+
+    enc = dict(models.CONFIGS["videoprism_v1_base"])
+    enc.update(num_spatial_layers=1, num_temporal_layers=1)
+    cls = models.get_model(None, model_fn=lambda: models.encoders.FactorizedVideoClassifier(encoder_params=enc,
+                                                                                          num_classes=5),
+                           fprop_dtype=dt)
+    kvar = params.synthetic_params(enc, 3, specs=cls.param_specs())
+    logits, kout = cls.apply(kvar, np.zeros((0, 2, 288, 288, 3), np.uint8), return_intermediate=True)
+    assert logits.shape == (0, 5) and kout["global_embeddings"].shape == (0, 768)

@@ -189,6 +189,8 @@ class Engine:
             fp = frame_paddings.to(device=video.device, dtype=torch.float32).contiguous()
             if tuple(fp.shape) != (B, T):
                 raise AssertionError(f"frame_paddings.shape == {(B, T)} failed (encoders.py:442)")
+        if B == 0:  # an empty batch: the reference's zero-size result, nothing to launch
+            return out, sp
         ws = self.workspace(B, T, H, W)
         s = stream if stream is not None else torch.cuda.current_stream(video.device)
         _native.call("vp_forward", self._h, ctypes.c_void_p(video.data_ptr()), in_dt, B, T, H, W,
@@ -400,6 +402,8 @@ class ClipEngine:
             fp = frame_paddings.to(device=dev, dtype=torch.float32).contiguous()
             if tuple(fp.shape) != (B, T):
                 raise AssertionError(f"frame_paddings.shape == {(B, T)} failed (encoders.py:442)")
+        if B == 0:  # an empty batch: zero-size embeddings, nothing to launch
+            return vemb, femb, sp, st
         n = ctypes.c_size_t()
         _native.call("vp_clip_video_workspace_bytes", self._h, B, T, H, W, ctypes.byref(n))
         ws = self._workspace("video", n.value)
@@ -421,6 +425,8 @@ class ClipEngine:
             raise ValueError(f"text_paddings must be [{Q}, {L}], got {tuple(pad.shape)}")
         D = self.cfg["model_dim"]
         out = torch.empty((Q, D), dtype=torch.float32, device=ids.device)
+        if Q == 0 and L >= 1:  # no queries: a zero-size result, nothing to launch
+            return out
         n = ctypes.c_size_t()
         _native.call("vp_clip_text_workspace_bytes", self._h, Q, L, ctypes.byref(n))
         ws = self._workspace("text", n.value)
@@ -629,6 +635,8 @@ class ClassifierEngine:
             fp = frame_paddings.to(device=dev, dtype=torch.float32).contiguous()
             if tuple(fp.shape) != (B, T):
                 raise AssertionError(f"frame_paddings.shape == {(B, T)} failed (encoders.py:442)")
+        if B == 0:  # an empty batch: zero-size logits, nothing to launch
+            return logits, emb, sp, st
         n = ctypes.c_size_t()
         _native.call("vp_classifier_workspace_bytes", self._h, B, T, H, W, ctypes.byref(n))
         if self._ws is None or self._ws.numel() < n.value:
