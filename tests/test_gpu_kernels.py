@@ -351,6 +351,37 @@ def test_attention_f32(cuda, S, num_seq, heads):
     assert np.abs(out.double().cpu().numpy() - ref).max() < 3e-5
 
 
+@pytest.mark.parametrize("S,num_seq,heads,scale,pad,cap", [
+    (256, 5, 12, 1.0, None, 50.0), (256, 5, 16, 0.125, None, 50.0), (256, 5, 12, 4.0, "frame", 50.0),
+    (256, 5, 16, 1.0, "random", 50.0), (256, 3, 12, 2.0, "random", 80.0), (256, 3, 12, 1.0, None, 0.0),
+    (128, 4, 12, 1.0, "random", 50.0), (200, 3, 16, 1.0, None, 50.0), (300, 2, 12, 1.0, "random", 50.0),
+    (520, 2, 12, 2.0, None, 50.0), (1000, 1, 16, 0.5, "random", 50.0), (2048, 1, 12, 1.0, None, 50.0),
+    (300, 2, 12, 1.0, None, 0.0)])
+def test_attention_f32_mfma(cuda, S, num_seq, heads, scale, pad, cap):
+    """fp32 attention (fprop_dtype=float32): S >= 128 with 0 < cap <= 50 takes the MFMA kernel
+    (attn_f32_mfma_kernel: 256-query blocks, 128-key chunks, a partial last block / chunk when S % 256 != 0),
+    cap 80 / no cap the generic online-softmax kernels; key paddings as the reference's
+    where(mask, logits, -0.7 FLT_MAX): a padded frame (every key: uniform weights) or random keys with one
+    fully padded sequence.  Against the fp64 oracle; bar 3e-5 relative to max(1, |o|), test_attention_f32's:
+    logits reach |q.k| ~ 100 at scale 2 - 4, where the fp32 rounding of the logit alone moves a probability
+    ~1e-5 relative."""
+    qkv = _qkv(num_seq, S, heads, 31 + heads + S, scale).to(cuda)
+    kp = None
+    if pad == "frame":
+        kp = torch.zeros(num_seq, S)
+        kp[2] = 1.0
+    elif pad == "random":
+        g = torch.Generator(device="cpu").manual_seed(5)
+        kp = (torch.rand(num_seq, S, generator=g) < 0.3).float()
+        kp[-1] = 1.0
+    out = nat.op_attention(qkv, num_seq, S, heads, cap, key_pad=None if kp is None else kp.reshape(-1).to(cuda))
+    torch.cuda.synchronize()
+    ref = _oracle_attention(qkv, num_seq, S, heads, cap, kp)
+    err = np.abs(out.double().cpu().numpy() - ref)
+    print(f"f32 S={S} heads {heads} scale {scale} pad {pad} cap {cap}: max-abs {err.max():.3e}")
+    assert np.all(err <= 3e-5 * np.maximum(1.0, np.abs(ref))), err.max()
+
+
 @pytest.mark.parametrize("D,perm", [(768, nat.PERM_NONE), (768, nat.PERM_BTN_TO_BNT),
                                     (1024, nat.PERM_BNT_TO_BTN)])
 @pytest.mark.parametrize("out_bf16", [False, True])

@@ -16,7 +16,8 @@
 //   ds_read_b64_tr_b16), so P never touches LDS and the row sum is lane-local.
 // attention_temporal_bf16: S = T <= 16 frames.  One wave per (sequence, head), 16x16x32 for
 //   Q.K^T and 16x16x16 for P.V; memory-bound on the qkv rows.
-// attention_f32: generic fp32 path (fprop_dtype=float32), online softmax, exact tanhf/expf.
+// attention_f32: fp32 path (fprop_dtype=float32): S = 256 with 0 < cap <= 50 on v_mfma_f32_32x32x2f32
+//   (attn_f32_mfma_kernel), any other S <= 256 / cap on a generic online-softmax kernel; exact tanhf/expf.
 #include <type_traits>
 
 #include "vp_common.h"
@@ -598,6 +599,145 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
         make_float4(acc[d] * inv, acc[d + 1] * inv, acc[d + 2] * inv, acc[d + 3] * inv);
 }
 
+// ------------------------------------------------------------------------------------
+// fp32 (fprop_dtype=float32, the reference's default precision) on v_mfma_f32_32x32x2f32, any S: the
+// spatial attention (S = 256), other patch grids (S >= 128), long clips' temporal attention and the LvT
+// auxiliary encoder (S = T*N).  Exact fp32 products summed in fp32; the numerators exp(cap * tanh(x / cap))
+// with the same tanhf / expf as attn_f32_kernel.  With 0 < cap <= 50 every capped logit lies in [-cap, cap],
+// so the softmax needs no running max (the bf16 kernels' argument, vp_internal.h kMaxFastCap).
+// A workgroup owns 256 queries of one (sequence, head), 8 waves x 32 queries; K and V stream through LDS in
+// 128-key chunks, double-buffered (chunk c + 1's loads in flight in registers while chunk c is consumed; one
+// barrier per chunk), rows padded to 68 floats so the b128 K reads and the b64 V reads are conflict-free.
+// S^T = K.Q^T puts one query per lane column; the contraction index d is permuted per lane half
+// (d = 32 (l / 32) + step) so a lane's K operands are 32 consecutive floats of its key row.  O^T = V^T.P^T
+// takes the numerators straight from the S^T accumulators: MFMA step r sums keys 8 (r / 4) + 4 (l / 32) + r % 4
+// -- the keys register r of each lane half holds -- and output row i of block b is d = 2 i + b, so a lane's
+// V operands are one 8-byte read.  Padded keys (MASK) weigh 0, a fully padded sequence gives uniform weights
+// (as attn_f32_kernel); TAIL (S % 256 != 0): query and key rows past S read row S - 1, keys past S weigh 0,
+// queries past S are not stored.
+// ------------------------------------------------------------------------------------
+constexpr int kF32Chunk = 128, kF32Row = 68;
+constexpr int kF32BufFloats = 2 * kF32Chunk * kF32Row + kF32Chunk;  // K, V, key paddings of one chunk
+constexpr int kF32MfmaLds = 2 * kF32BufFloats * 4 + 16;
+
+template <bool MASK, bool TAIL>
+__global__ __launch_bounds__(512) void attn_f32_mfma_kernel(const float* __restrict__ qkv, float* __restrict__ o,
+                                                            int S, int heads, int nqb, float cap,
+                                                            const float* __restrict__ key_pad) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* bufs = reinterpret_cast<float*>(smem);
+  const int D = heads * 64;
+  const int64_t ld = 3 * (int64_t)D;
+  const int qb = blockIdx.x % nqb;
+  const int sh = blockIdx.x / nqb;
+  const int seq = sh / heads;
+  const int h = sh % heads;
+  const float* base = qkv + (int64_t)seq * S * ld + h * 64;
+  const int t = threadIdx.x, lane = t & 63, w = wave_id();
+  const int half = lane >> 5, l32 = lane & 31;
+  const int q = qb * 256 + 32 * w + l32;
+
+  // this wave's 32 queries as the B operand: lane l holds Q[q][32 (l / 32) + s], s = 0..31
+  float qf[32];
+  {
+    const float* qp = base + (int64_t)(TAIL ? min(q, S - 1) : q) * ld + 32 * half;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 v = *reinterpret_cast<const float4*>(qp + 4 * i);
+      qf[4 * i] = v.x; qf[4 * i + 1] = v.y; qf[4 * i + 2] = v.z; qf[4 * i + 3] = v.w;
+    }
+  }
+  bool all_masked = false;
+  if constexpr (MASK) {
+    int valid = 0;
+    for (int i = t; i < S; i += 512) valid |= key_pad[(int64_t)seq * S + i] == 0.0f;
+    all_masked = __syncthreads_or(valid) == 0;
+  }
+  // chunk c: 128 key rows x 16 float4 of K and of V, 4 of each per thread (+ the chunk's key paddings)
+  f32x4 kr[4], vr[4];  // (native vectors: arrays of HIP's float4 struct stay in scratch here)
+  float pr = 0.0f;
+  auto stage = [&](int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = t + 512 * i, row = idx >> 4, c4 = (idx & 15) * 4;
+      const int key = TAIL ? min(c * kF32Chunk + row, S - 1) : c * kF32Chunk + row;
+      kr[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)key * ld + D + c4);
+      vr[i] = *reinterpret_cast<const f32x4*>(base + (int64_t)key * ld + 2 * D + c4);
+    }
+    if constexpr (MASK) {
+      const int key = c * kF32Chunk + t;
+      if (t < kF32Chunk) pr = key < S ? key_pad[(int64_t)seq * S + key] : 1.0f;
+    }
+  };
+  auto store = [&](int c) __attribute__((always_inline)) {
+    float* Kb = bufs + (c & 1) * kF32BufFloats;
+    float* Vb = Kb + kF32Chunk * kF32Row;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = t + 512 * i, row = idx >> 4, c4 = (idx & 15) * 4;
+      *reinterpret_cast<f32x4*>(Kb + row * kF32Row + c4) = kr[i];
+      *reinterpret_cast<f32x4*>(Vb + row * kF32Row + c4) = vr[i];
+    }
+    if constexpr (MASK) {
+      if (t < kF32Chunk) Vb[kF32Chunk * kF32Row + t] = pr;
+    }
+  };
+
+  f32x16 y0 = {}, y1 = {};  // O^T blocks b = 0 / 1: row i <-> d = 2 i + b
+  float lsum = 0.0f;
+  const int nch = (S + kF32Chunk - 1) / kF32Chunk;
+  stage(0);
+  store(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) stage(c + 1);  // in flight while chunk c is consumed
+    const float* Kb = bufs + (c & 1) * kF32BufFloats;
+    const float* Vb = Kb + kF32Chunk * kF32Row;
+    const float* kp = Vb + kF32Chunk * kF32Row;
+#pragma unroll 1
+    for (int kt = 0; kt < kF32Chunk / 32; ++kt) {
+      // S^T tile: x[r] = logit(key c 128 + kt 32 + 8 (r / 4) + 4 half + r % 4, query q)
+      f32x16 x = {};
+      const float* kq = Kb + (kt * 32 + l32) * kF32Row + 32 * half;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 kv = *reinterpret_cast<const float4*>(kq + 4 * i);
+        x = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qf[4 * i], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qf[4 * i + 1], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qf[4 * i + 2], x, 0, 0, 0);
+        x = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qf[4 * i + 3], x, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kl = kt * 32 + 8 * (r >> 2) + 4 * half + (r & 3);  // key within the chunk
+        float e = expf(cap * tanhf(x[r] / cap));
+        if constexpr (MASK) e = all_masked ? 1.0f : (kp[kl] != 0.0f ? 0.0f : e);
+        if constexpr (TAIL) e = c * kF32Chunk + kl < S ? e : 0.0f;
+        lsum += e;
+        const float2 vv = *reinterpret_cast<const float2*>(Vb + kl * kF32Row + 2 * l32);
+        y0 = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.x, e, y0, 0, 0, 0);
+        y1 = __builtin_amdgcn_mfma_f32_32x32x2f32(vv.y, e, y1, 0, 0, 0);
+      }
+    }
+    // buffer (c + 1) & 1 was last read in chunk c - 1, before the previous barrier
+    if (c + 1 < nch) store(c + 1);
+    __syncthreads();
+  }
+  lsum += __shfl_xor(lsum, 32);
+  const float inv = 1.0f / lsum;
+  if (TAIL && q >= S) return;
+  // y_b[4 m + c] = O[q][d = 16 m + 8 half + 2 c + b]: 8 consecutive floats per m
+  float* op = o + ((int64_t)seq * S + q) * D + h * 64 + 8 * half;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    *reinterpret_cast<float4*>(op + 16 * m) =
+        make_float4(y0[4 * m] * inv, y1[4 * m] * inv, y0[4 * m + 1] * inv, y1[4 * m + 1] * inv);
+    *reinterpret_cast<float4*>(op + 16 * m + 4) =
+        make_float4(y0[4 * m + 2] * inv, y1[4 * m + 2] * inv, y0[4 * m + 3] * inv, y1[4 * m + 3] * inv);
+  }
+}
+
 }  // namespace
 
 hipError_t attention_spatial_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int heads, float cap,
@@ -667,9 +807,39 @@ hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, 
   return hipGetLastError();
 }
 
+hipError_t attention_f32_mfma(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
+                              const float* key_pad, hipStream_t s) {
+  if (!(cap > 0.0f && cap <= 50.0f)) return hipErrorNotSupported;
+  if (S < 1 || num_seq < 1 || heads < 1) return hipErrorInvalidValue;
+  const int nqb = (S + 255) / 256;
+  const int64_t grid = (int64_t)num_seq * heads * nqb;
+  if (grid > 0x7fffffff || (int64_t)num_seq * S > 0x7fffffff) return hipErrorInvalidValue;
+  const int mi = (key_pad ? 1 : 0) + (S % 256 ? 2 : 0);
+  const void* fns[4] = {(const void*)attn_f32_mfma_kernel<false, false>, (const void*)attn_f32_mfma_kernel<true, false>,
+                        (const void*)attn_f32_mfma_kernel<false, true>, (const void*)attn_f32_mfma_kernel<true, true>};
+  hipError_t e = ensure_dyn_lds(fns[mi], kF32MfmaLds);
+  if (e != hipSuccess) return e;
+  VP_NOTE_KERNEL(fns[mi]);
+#define VP_F32M(M, T)                                                                                              \
+  hipLaunchKernelGGL((attn_f32_mfma_kernel<M, T>), dim3((unsigned)grid), dim3(512), kF32MfmaLds, s, qkv, o, S, heads, \
+                     nqb, cap, key_pad)
+  switch (mi) {
+    case 0: VP_F32M(false, false); break;
+    case 1: VP_F32M(true, false); break;
+    case 2: VP_F32M(false, true); break;
+    default: VP_F32M(true, true); break;
+  }
+#undef VP_F32M
+  return hipGetLastError();
+}
+
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
                          const float* key_pad, hipStream_t s) {
   if (S < 1 || S > kF32MaxS) return hipErrorInvalidValue;
+  if (S >= 128) {  // MFMA kernel (max-free softmax: 0 < cap <= 50); other caps fall through to the generic one
+    const hipError_t e = attention_f32_mfma(qkv, o, num_seq, S, heads, cap, key_pad, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   const int lds = (2 * S * 64 + S) * 4 + 16;
   hipError_t e = ensure_dyn_lds((const void*)attn_f32_kernel, (2 * kF32MaxS * 64 + kF32MaxS) * 4 + 16);
   if (e != hipSuccess) return e;

@@ -644,8 +644,15 @@ int vp_op_attention(int precision, const void* qkv, void* o, int64_t num_seq, in
     else
       return fail(VP_EINVAL, "bad S");
   } else if (precision == VP_F32) {
-    if (S < 1 || S > 256) return fail(VP_ENOTSUP, "fp32 attention supports S <= 256");
-    VP_HIP(attention_f32((const float*)qkv, (float*)o, (int)num_seq, (int)S, (int)heads, cap, key_pad, s));
+    if (S < 1) return fail(VP_EINVAL, "bad S");
+    if (S <= 256) {
+      VP_HIP(attention_f32((const float*)qkv, (float*)o, (int)num_seq, (int)S, (int)heads, cap, key_pad, s));
+    } else {  // the forward's choice for long sequences (run_stack): the MFMA kernel, else online softmax
+      const hipError_t e = attention_f32_mfma((const float*)qkv, (float*)o, (int)num_seq, (int)S, (int)heads, cap,
+                                              key_pad, s);
+      if (e != hipErrorNotSupported) VP_HIP(e);
+      else VP_HIP(attention_masked(qkv, o, 0, (int)num_seq, (int)S, (int)heads, cap, key_pad, 0, s));
+    }
   } else {
     return fail(VP_EINVAL, "bad precision");
   }

@@ -626,6 +626,12 @@ struct Fwd {
         VP_HIP(rec(PC_GEMM_QKV, 2.0 * dM * dD * 3 * dD, gbytes(dD, 3 * dD, dE, 0), [&] {
           return gemm(EPI_BF16, hb, D, lw.wqkv, 3 * D, big, 3 * D, lw.bqkv, nullptr, nullptr, 1, nullptr); }));
       }
+      // fp32 sequences longer than 256 (the auxiliary encoder, long clips' temporal attention, large patch grids): the
+      // MFMA kernel for 0 < cap <= 50, else the generic online-softmax one
+      auto attention_f32_long = [&](int ns, int len, const float* kpad) {
+        const hipError_t e = attention_f32_mfma((const float*)big, (float*)hb, ns, len, NH, cap, kpad, s);
+        return e != hipErrorNotSupported ? e : attention_masked(big, hb, 0, ns, len, NH, cap, kpad, 0, s);
+      };
       if (!tattn) VP_HIP(rec(acls, aflops, abytes, [&] {
         if (kind == ATT_TEXT) {
           if (bf && fast_cap(cap) && S > 16 && S <= 256)
@@ -636,7 +642,7 @@ struct Fwd {
         // layers.py:586-589) or a larger cap runs the online-softmax kernel
         if (bf && !fast_cap(cap)) return attention_masked(big, hb, 1, num_seq, S, NH, cap, pad, 0, s);
         if (kind == ATT_LONG) {  // no masks (encoders.py:855); any T*N
-          if (!bf) return attention_masked(big, hb, 0, num_seq, S, NH, cap, nullptr, 0, s);
+          if (!bf) return attention_f32_long(num_seq, S, nullptr);
           if (S >= 256) return attention_long_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, s);
           if (S > 16) return attention_seq_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, nullptr, s);
           return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, nullptr, s);
@@ -645,7 +651,7 @@ struct Fwd {
         // on the generic fp32-math kernel
         if (!bf) {
           if (S <= 256) return attention_f32((const float*)big, (float*)hb, num_seq, S, NH, cap, pad, s);
-          return attention_masked(big, hb, 0, num_seq, S, NH, cap, pad, 0, s);
+          return attention_f32_long(num_seq, S, pad);
         }
         if (S == 256) return attention_spatial_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, NH, cap, pad, s, sblk);
         if (S <= 16) return attention_temporal_bf16((const bf16_t*)big, (bf16_t*)hb, num_seq, S, NH, cap, pad, s);

@@ -138,8 +138,13 @@ hipError_t attention_seq_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, 
                               const float* key_pad, hipStream_t s, int causal = 0);
 hipError_t attention_temporal_bf16(const bf16_t* qkv, bf16_t* o, int num_seq, int S, int heads,
                                    float cap, const float* key_pad, hipStream_t s);
+// fp32, S <= 256: S >= 128 with 0 < cap <= 50 on the MFMA (attention_f32_mfma), else the generic kernel
 hipError_t attention_f32(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
                          const float* key_pad, hipStream_t s);
+// fp32 on v_mfma_f32_32x32x2f32, any S, no causal mask: hipErrorNotSupported unless 0 < cap <= 50 (the
+// max-free softmax); the callers then take the generic online-softmax kernels
+hipError_t attention_f32_mfma(const float* qkv, float* o, int num_seq, int S, int heads, float cap,
+                              const float* key_pad, hipStream_t s);
 
 // ---- elementwise / normalisation (elementwise.hip) ----
 enum RowPerm { PERM_NONE = 0, PERM_BTN_TO_BNT = 1, PERM_BNT_TO_BTN = 2 };
