@@ -694,3 +694,35 @@ def test_patch_embed_fused_rejects_odd_patch(cuda):
     out = torch.empty(256, D, device=cuda, dtype=torch.bfloat16)
     with pytest.raises(ValueError, match="even patch size"):
         nat.dev_patch_embed(v, P, wv, torch.zeros(D, device=cuda), torch.zeros(256, D, device=cuda), out)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (1024, 2304, 768), (384, 256, 3072), (1280, 640, 16)])
+@pytest.mark.parametrize("epi", [nat.EPI_STORE, nat.EPI_GELU, nat.EPI_RESID, nat.EPI_POS, nat.EPI_RESID_FFN])
+def test_gemm_f32_kernels(cuda, M, N, K, epi):
+    """Both fp32 GEMM kernels (round 1's 16x16x4 one, which = 32, and the 32x32x2 product kernel, 33) on
+    every fp32 epilogue, odd tile counts (XCD-contiguous ranges need a grid % 8 == 0) and a single K-tile,
+    against fp64: exact fp32 products, fp32 sums in different orders, so each within 2e-5 of fp64."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + epi)
+    a = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    pad = (torch.rand(M, generator=g) < 0.25).float().to(cuda)
+    x0 = torch.randn(M, N, generator=g).to(cuda)
+    pos = torch.randn(256, N, generator=g).to(cuda) if epi == nat.EPI_POS else None
+    y = a.double() @ w.double().T + b.double()
+    keep = (1 - pad.double())[:, None]
+    if epi == nat.EPI_GELU:
+        ref = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) * keep
+    elif epi in (nat.EPI_RESID, nat.EPI_RESID_FFN):
+        ref = x0.double() + y * keep
+    elif epi == nat.EPI_POS:
+        ref = y + pos.double().repeat(M // 256 + 1, 1)[:M]
+    else:
+        ref = y
+    for which in (32, 33):
+        o = x0.clone()
+        nat.dev_gemm_kernel(which, a, w, b, epi, o, resid=o if epi in (nat.EPI_RESID, nat.EPI_RESID_FFN) else None,
+                            pos=pos, rowpad=pad if epi != nat.EPI_POS and epi != nat.EPI_STORE else None)
+        torch.cuda.synchronize()
+        err = float((o.double() - ref).abs().max())
+        assert err < 2e-5, (which, err)

@@ -37,7 +37,7 @@ __device__ __forceinline__ bf16x8 rand_frag(uint32_t seed) {
   return v;
 }
 
-template <int SHAPE>  // 0: 16x16x32, 1: 32x32x16
+template <int SHAPE>  // 0: 16x16x32 bf16, 1: 32x32x16 bf16, 2: 16x16x4 f32, 3: 32x32x2 f32
 __global__ __launch_bounds__(256) void mfma_peak_kernel(int iters, float* sink, unsigned long long* stamps) {
   const uint32_t gid = blockIdx.x * 256u + threadIdx.x;
   const bf16x8 a = rand_frag(gid * 2u + 1u), b = rand_frag(gid * 2u + 2u);
@@ -60,6 +60,31 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(int iters, float* sink, 
     }
     const f32x4 t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
     s = t[0] + t[1] + t[2] + t[3];
+  } else if constexpr (SHAPE == 2) {  // fp32 operands: one random float per lane in about [-1, 1)
+    const float fa = __uint_as_float((hash32(gid * 2u + 1u) & 0x807fffffu) | 0x3f000000u);
+    const float fb = __uint_as_float((hash32(gid * 2u + 2u) & 0x807fffffu) | 0x3f000000u);
+    f32x4 a0 = {0.f}, a1 = {1.f}, a2 = {2.f}, a3 = {3.f}, a4 = {4.f}, a5 = {5.f}, a6 = {6.f}, a7 = {7.f};
+#pragma unroll 1
+    for (int it = 0; it < iters; ++it) {
+#define VP_F16(acc) asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(fa), "v"(fb))
+      VP_F16(a0); VP_F16(a1); VP_F16(a2); VP_F16(a3); VP_F16(a4); VP_F16(a5); VP_F16(a6); VP_F16(a7);
+#undef VP_F16
+    }
+    const f32x4 t = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+    s = t[0] + t[1] + t[2] + t[3];
+  } else if constexpr (SHAPE == 3) {
+    const float fa = __uint_as_float((hash32(gid * 2u + 1u) & 0x807fffffu) | 0x3f000000u);
+    const float fb = __uint_as_float((hash32(gid * 2u + 2u) & 0x807fffffu) | 0x3f000000u);
+    f32x16 a0 = {0.f}, a1 = {1.f}, a2 = {2.f}, a3 = {3.f};
+#pragma unroll 1
+    for (int it = 0; it < iters; ++it) {
+#define VP_F32(acc) asm volatile("v_mfma_f32_32x32x2_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(fa), "v"(fb))
+      VP_F32(a0); VP_F32(a1); VP_F32(a2); VP_F32(a3);
+#undef VP_F32
+    }
+    const f32x16 t = a0 + a1 + a2 + a3;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += t[j];
   } else {
     f32x16 a0 = {0.f}, a1 = {1.f}, a2 = {2.f}, a3 = {3.f};
 #pragma unroll 1
@@ -85,12 +110,14 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(int iters, float* sink, 
 
 extern "C" {
 
-// shape 0: v_mfma_f32_16x16x32_bf16, 1: v_mfma_f32_32x32x16_bf16.  Runs `reps` timed launches of `iters`
+// shape 0: v_mfma_f32_16x16x32_bf16, 1: v_mfma_f32_32x32x16_bf16, 2: v_mfma_f32_16x16x4_f32 (the fp32 GEMMs'),
+// 3: v_mfma_f32_32x32x2_f32 (the fp32 attention's).  Runs `reps` timed launches of `iters`
 // loop iterations after one warm-up launch on every CU of device `device`; writes the best and the median
 // TFLOP/s, the median in-kernel clock (GHz) over the workgroups of the last launch, and the ms per launch.
 // Returns 0 or a hipError_t.
 int mfma_peak_run(int device, int shape, int iters, int reps, double* tflops_best, double* tflops_median,
                   double* clock_ghz, double* ms_median) {
+  if (shape < 0 || shape > 3) return hipErrorInvalidValue;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return e;
   int cus = 0;
@@ -103,14 +130,19 @@ int mfma_peak_run(int device, int shape, int iters, int reps, double* tflops_bes
   hipEventCreate(&a);
   hipEventCreate(&b);
   // FLOPs per MFMA: 2 * 16 * 16 * 32 = 16384 (8 per iteration) or 2 * 32 * 32 * 16 = 32768 (4 per iteration)
-  const double flops = (double)cus * 4 * iters * (shape == 0 ? 8.0 * 16384.0 : 4.0 * 32768.0);
+  const double per_iter[4] = {8.0 * 16384.0, 4.0 * 32768.0, 8.0 * 2048.0, 4.0 * 4096.0};
+  const double flops = (double)cus * 4 * iters * per_iter[shape];
   std::vector<double> tf;
   for (int r = 0; r <= reps && e == hipSuccess; ++r) {
     hipEventRecord(a, nullptr);
     if (shape == 0)
       hipLaunchKernelGGL(mfma_peak_kernel<0>, dim3(cus), dim3(256), 0, nullptr, iters, sink, stamps);
-    else
+    else if (shape == 1)
       hipLaunchKernelGGL(mfma_peak_kernel<1>, dim3(cus), dim3(256), 0, nullptr, iters, sink, stamps);
+    else if (shape == 2)
+      hipLaunchKernelGGL(mfma_peak_kernel<2>, dim3(cus), dim3(256), 0, nullptr, iters, sink, stamps);
+    else
+      hipLaunchKernelGGL(mfma_peak_kernel<3>, dim3(cus), dim3(256), 0, nullptr, iters, sink, stamps);
     hipEventRecord(b, nullptr);
     e = hipEventSynchronize(b);
     float ms = 0.f;

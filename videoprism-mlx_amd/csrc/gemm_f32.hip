@@ -126,12 +126,110 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   }
 }
 
+// ---- v2 (round 6): v_mfma_f32_32x32x2_f32, K-tile 16 with a per-lane-half k permutation ----
+// Same 128x128 workgroup tile and 2x2 waves of 64x64, but on 32x32x2 MFMAs (2 x 2 blocks per wave, 32 MFMAs
+// per K-tile instead of 64) with operands read as whole 16-B runs: in K-tile step s (0..7) lane half h
+// contracts k = 8 h + s, so a lane's 8 operands of a K-tile are 8 consecutive floats of its row (two
+// ds_read_b128 per row) and the LDS tiles keep the global row-major layout ([row][16 k], rows padded to 20
+// floats: conflict-free b128 reads, plain float4 copies in, no transposition).  Operands swapped as in v1
+// (D^T = W.A^T): register r of block (nb, mb) is output row m = l % 32, column n = 8 (r / 4) + 4 (l / 32) + r % 4,
+// so each lane owns 4 consecutive columns of one row for the 16-byte epilogue stores.  XCD-contiguous tile
+// ranges (workgroup b runs on XCD b % 8), M-block-major inside a range so an A block stays in its XCD's L2
+// across the N tiles.  Exact fp32 products summed in fp32 (another order than v1: k-pairs, then steps).
+// Measured (tools/gemm_f32_ab.py, Base B = 4 shapes, profiles/r06/fp32_gemm_ab.txt): 1-5 % faster than v1
+// (ffn2 593.7 vs 624.5 us); a K-tile of 32 (73.7 KB of LDS: two workgroups per CU) was 8-38 % slower.
+template <int EPI, int TK2 = 16>
+__global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict__ A, int64_t lda,
+                                                        const float* __restrict__ W, int64_t ldw,
+                                                        int M, int N, int K, EpiArgs ep) {
+  constexpr int ROW2 = TK2 + 4, SPR = TK2 / 4;  // row stride (floats), float4 per row
+  constexpr int NST = TM * SPR / 256;            // float4 of A (and of W) per thread per K-tile
+  constexpr int SH = TK2 / 2;                     // steps per K-tile (k = SH h + s)
+  __shared__ __attribute__((aligned(16))) float lds[2][2][TM * ROW2];  // [buffer][A | W][row][k]
+  const int tilesN = N / TN;
+  int bid = (int)blockIdx.x;
+  if (gridDim.x % 8 == 0) bid = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
+  const int m0 = (bid / tilesN) * TM, n0 = (bid % tilesN) * TN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+  // staging: 128 rows x SPR float4 of A and of W per K-tile, NST of each per thread
+  f32x4 ra[NST], rw[NST];
+  auto gload = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = t + 256 * i, row = idx / SPR, c4 = (idx % SPR) * 4;
+      ra[i] = *reinterpret_cast<const f32x4*>(A + (int64_t)(m0 + row) * lda + k0 + c4);
+      rw[i] = *reinterpret_cast<const f32x4*>(W + (int64_t)(n0 + row) * ldw + k0 + c4);
+    }
+  };
+  auto sstore = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = t + 256 * i, row = idx / SPR, c4 = (idx % SPR) * 4;
+      *reinterpret_cast<f32x4*>(&lds[buf][0][row * ROW2 + c4]) = ra[i];
+      *reinterpret_cast<f32x4*>(&lds[buf][1][row * ROW2 + c4]) = rw[i];
+    }
+  };
+  f32x16 acc[2][2];  // [n block][m block]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  const int nk = K / TK2;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * TK2);
+    f32x4 av[2][SH / 4], wv[2][SH / 4];  // [block][k SH h + 4 j .. + 3]
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < SH / 4; ++j) {
+        av[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][0][(wm * 64 + b * 32 + l32) * ROW2 + SH * half + 4 * j]);
+        wv[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][1][(wn * 64 + b * 32 + l32) * ROW2 + SH * half + 4 * j]);
+      }
+#pragma unroll
+    for (int st = 0; st < SH; ++st)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+          acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[nb][st >> 2][st & 3], av[mb][st >> 2][st & 3],
+                                                             acc[nb][mb], 0, 0, 0);
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = n0 + wn * 64 + nb * 32 + 8 * q + 4 * half;
+      const float4 b = *reinterpret_cast<const float4*>(ep.bias + n);
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb) {
+        const f32x16& a = acc[nb][mb];
+        epi_f32<EPI>(ep, N, m0 + wm * 64 + mb * 32 + l32, n, a[4 * q] + b.x, a[4 * q + 1] + b.y,
+                     a[4 * q + 2] + b.z, a[4 * q + 3] + b.w);
+      }
+    }
+}
+
 template <int EPI>
 hipError_t launch(const float* A, int64_t lda, const float* W, int64_t ldw, int M, int N, int K,
-                  const EpiArgs& ep, hipStream_t s) {
-  VP_NOTE_KERNEL(gemm_f32_kernel<EPI>);
-  hipLaunchKernelGGL(gemm_f32_kernel<EPI>, dim3((M / TM) * (N / TN)), dim3(256), 0, s, A, lda, W,
-                     ldw, M, N, K, ep);
+                  const EpiArgs& ep, hipStream_t s, int version) {
+  if (version == 1) {
+    VP_NOTE_KERNEL(gemm_f32_kernel<EPI>);
+    hipLaunchKernelGGL(gemm_f32_kernel<EPI>, dim3((M / TM) * (N / TN)), dim3(256), 0, s, A, lda, W,
+                       ldw, M, N, K, ep);
+  } else {
+    VP_NOTE_KERNEL(gemm_f32_kernel2<EPI>);
+    hipLaunchKernelGGL(gemm_f32_kernel2<EPI>, dim3((M / TM) * (N / TN)), dim3(256), 0, s, A, lda, W,
+                       ldw, M, N, K, ep);
+  }
   return hipGetLastError();
 }
 
@@ -146,14 +244,14 @@ const char* gemm_f32_check(int M, int N, int K) {
 }
 
 hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_t ldw, int M, int N,
-                    int K, const EpiArgs& ep, hipStream_t s) {
+                    int K, const EpiArgs& ep, hipStream_t s, int version) {
   switch (epi) {
-    case EPI_BF16: return launch<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_F32: return launch<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_POS_F32: return launch<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RESID_FFN: return launch<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s);
-    case EPI_RELU_BF16: return launch<EPI_RELU_BF16>(A, lda, W, ldw, M, N, K, ep, s);
+    case EPI_BF16: return launch<EPI_BF16>(A, lda, W, ldw, M, N, K, ep, s, version);
+    case EPI_GELU_BF16: return launch<EPI_GELU_BF16>(A, lda, W, ldw, M, N, K, ep, s, version);
+    case EPI_RESID_F32: return launch<EPI_RESID_F32>(A, lda, W, ldw, M, N, K, ep, s, version);
+    case EPI_POS_F32: return launch<EPI_POS_F32>(A, lda, W, ldw, M, N, K, ep, s, version);
+    case EPI_RESID_FFN: return launch<EPI_RESID_FFN>(A, lda, W, ldw, M, N, K, ep, s, version);
+    case EPI_RELU_BF16: return launch<EPI_RELU_BF16>(A, lda, W, ldw, M, N, K, ep, s, version);
   }
   return hipErrorInvalidValue;
 }

@@ -522,7 +522,8 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
                        int64_t K, void* out, const float* bias, const void* resid, const float* pos,
                        int64_t pos_rows, const float* rowpad, void* stream) {
   using namespace vp;
-  const char* e = which == 1 ? nullptr : gemm_bf16_check((int)M, (int)N, (int)K, K, K);
+  const char* e = which == 1 ? nullptr : (which == 32 || which == 33) ? gemm_f32_check((int)M, (int)N, (int)K)
+                                                                       : gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;
   ep.out = out; ep.ldo = N; ep.bias = bias; ep.resid = resid; ep.ldr = N;
@@ -536,8 +537,10 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
     if (!gemm_bf16_small_ok(epi, (int)M, (int)N, (int)K, K, K))
       return fail(VP_EINVAL, "small-M GEMM: epilogue 0, 1, 2, 4, 5, 7 or 13 and K % 256 == 0");
     VP_HIP(gemm_bf16_small(epi, (const bf16_t*)A, K, (const bf16_t*)W, K, (int)M, (int)N, (int)K, ep, s));
+  } else if (which == 32 || which == 33) {  // fp32: round 1's 16x16x4 kernel (32) / the 32x32x2 kernel (33)
+    VP_HIP(gemm_f32(epi, (const float*)A, K, (const float*)W, K, (int)M, (int)N, (int)K, ep, s, which - 31));
   } else
-    return fail(VP_EINVAL, "which must be 1, 4 or 8");
+    return fail(VP_EINVAL, "which must be 1, 4, 8, 32 or 33");
   return VP_OK;
 }
 
