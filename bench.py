@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VideoPrism-Base bf16 forward throughput on MI355X (BASELINE.json metric/configs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload base|large|lvt_large|lvt_base]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload base|large|lvt_large|lvt_base] [--dtype bf16|f32]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -20,6 +20,9 @@ Also reported (one JSON line on rank 0):
                (the newest profiles/traffic_r*_<workload>.json whose source fingerprint matches,
                tools/pmc_traffic.sh), else null
   cpu_baseline the NumPy oracle (oracle/, fp32) on one clip on this host's cores (rank 0, N=1)
+
+`--dtype f32` measures the same step in fprop_dtype=float32 (the reference's default, `get_model(name)`), against
+the fp32 MFMA peak; the headline line is bf16.
 
 `--standin` replaces the GPU forward by a small CPU function (gloo backend) so the multi-process
 plumbing -- spawning, sharding, the gather's row order, the similarity shape, n_gpus -- can be
@@ -41,6 +44,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "videoprism-mlx_amd")]
 
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip parameters)
+PEAK_F32_TFLOPS = 157.3     # MI355X fp32 MFMA (--dtype f32: the reference's default precision)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E spec (same table)
 CPU_BASELINE_THREADS = 16   # the GPU box's CPU share per GPU
 
@@ -117,7 +121,7 @@ def cpu_baseline(cfg, variables, runs: int = 5, warmups: int = 2) -> dict:
             "runs_s": [round(t, 3) for t in times]}
 
 
-def measured_mfma_peak(device: int, iters: int = 4_000_000, reps: int = 3) -> dict | None:
+def measured_mfma_peak(device: int, iters: int = 4_000_000, reps: int = 3, f32: bool = False) -> dict | None:
     """The bf16 MFMA rate this GPU sustains with every CU issuing back-to-back MFMAs from registers on
     random operands (tools/peak/mfma_peak.hip): TFLOP/s (median of `reps` launches of
     ~0.25 s after a warm-up launch) and the in-kernel clock, for both MFMA shapes the kernels use.
@@ -128,9 +132,10 @@ def measured_mfma_peak(device: int, iters: int = 4_000_000, reps: int = 3) -> di
         return None
     lib = ctypes.CDLL(path)
     out = {}
-    for shape, key in ((0, "16x16x32"), (1, "32x32x16")):
+    shapes = ((2, "16x16x4f32"), (3, "32x32x2f32")) if f32 else ((0, "16x16x32"), (1, "32x32x16"))
+    for shape, key in shapes:
         best, med, clk, ms = (ctypes.c_double() for _ in range(4))
-        rc = lib.mfma_peak_run(device, shape, iters, reps, ctypes.byref(best),
+        rc = lib.mfma_peak_run(device, shape, iters // 4 if f32 else iters, reps, ctypes.byref(best),
                                ctypes.byref(med), ctypes.byref(clk), ctypes.byref(ms))
         if rc != 0:
             return None
@@ -277,6 +282,8 @@ def main() -> None:
     ap.add_argument("--workload", default="base", choices=sorted(WORKLOADS),
                     help="base = configs[1] (default, the headline metric); large = configs[2]; "
                          "lvt_large = configs[4] video+text")
+    ap.add_argument("--dtype", default="bf16", choices=("bf16", "f32"),
+                    help="compute dtype: bf16 (the headline, fprop_dtype=bfloat16) or f32 (the reference's default)")
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU")
     ap.add_argument("--queries", type=int, default=8, help="text queries (LvT workloads)")
     ap.add_argument("--frames", type=int, default=16)
@@ -351,7 +358,8 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
         local_dev = distributed.local_device(local_rank)
         torch.cuda.set_device(local_dev)
         dev = torch.device(f"cuda:{local_dev}")
-        model = models.get_model(name, fprop_dtype=torch.bfloat16)
+        f32 = args.dtype == "f32"
+        model = models.get_model(name, fprop_dtype=None if f32 else torch.bfloat16)
         if lvt:
             cfg["vocabulary_size"] = model.vocabulary_size
             variables = params.synthetic_params(cfg, seed=0, specs=params.clip_leaf_specs(cfg))
@@ -360,7 +368,9 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
         eng = model.engine(variables, local_dev)
         ops = GpuOps(eng, _native)
         gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-        video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev).to(torch.bfloat16)
+        video = torch.rand((B, T, 288, 288, 3), generator=gen, device=dev)
+        if not f32:
+            video = video.to(torch.bfloat16)
         comm = distributed.Communicator(local_dev) if gather else None
         if comm is not None:
             owned.append(comm)
@@ -384,7 +394,7 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
             last["rows"], last["sim"] = vemb, ops.similarity(vemb, temb)
     else:
         out = torch.empty((B, T * 256, cfg["model_dim"]),
-                          dtype=torch.float32 if args.standin else torch.bfloat16, device=dev)
+                          dtype=torch.float32 if args.standin or args.dtype == "f32" else torch.bfloat16, device=dev)
 
         def step():
             ops.forward(video, out)
@@ -431,6 +441,7 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
     gpc = lvt_gflop_per_clip(cfg, T) if lvt else gflop_per_clip(cfg, T)
     text_gf = text_gflop_per_query(cfg) * args.queries if lvt else 0.0
 
+    peak_tf = PEAK_F32_TFLOPS if args.dtype == "f32" else PEAK_BF16_TFLOPS
     roofline = None
     kernel_ms = {}
     if prof:
@@ -448,8 +459,8 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
                 break
         if dom["flops"] > 0:
             ach = dom["flops"] / dom["launches"] / avg_s / 1e12
-            roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+            roofline = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak_tf,
+                        "unit": "TFLOP/s", "frac": round(ach / peak_tf, 4),
                         "traffic": traffic}
         else:
             ach = dom["bytes"] / dom["launches"] / avg_s / 1e9
@@ -466,17 +477,24 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
     if roofline is not None and rank == 0 and not args.no_peak:
         # the spec peak beside the peak this GPU sustains (bare MFMAs from registers, all CUs, random data):
         # the GEMMs issue v_mfma_f32_16x16x32_bf16, the attention kernels v_mfma_f32_32x32x16_bf16
-        pk = measured_mfma_peak(dev.index if dev.index is not None else 0) if roofline["bound"] == "mfma" else None
+        f32 = args.dtype == "f32"
+        pk = (measured_mfma_peak(dev.index if dev.index is not None else 0, f32=f32)
+              if roofline["bound"] == "mfma" else None)
         if pk is not None:
-            shape = "16x16x32" if "gemm" in (dom_symbol or "") else "32x32x16"
+            if f32:  # the fp32 GEMMs and attention both issue v_mfma_f32_32x32x2_f32
+                shape = "32x32x2f32"
+            else:
+                shape = "16x16x32" if "gemm" in (dom_symbol or "") else "32x32x16"
             pm = pk[shape]["tflops"]
             roofline.update({"peak_measured": pm, "frac_measured": round(roofline["achieved"] / pm, 4),
-                             "peak_measured_shape": f"v_mfma_f32_{shape}_bf16",
+                             "peak_measured_shape": (f"v_mfma_f32_{shape[:-3]}_f32" if f32 else
+                                                     f"v_mfma_f32_{shape}_bf16"),
                              "peak_measured_clock_ghz": pk[shape]["clock_ghz"],
                              "peak_measured_all": pk,
                              "peak_measured_source": "tools/peak/mfma_peak.hip: one 256-thread workgroup per CU, "
-                                                     "back-to-back MFMAs from registers, random bf16, after the "
-                                                     "timed region; median of 3 launches"})
+                                                     "back-to-back MFMAs from registers, random "
+                                                     f"{'fp32' if f32 else 'bf16'} operands, after the timed region; "
+                                                     "median of 3 launches"})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not lvt and not args.standin:
@@ -500,23 +518,23 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
         label = {"base": "VideoPrism-Base fwd", "large": "VideoPrism-Large fwd",
                  "lvt_large": "VideoPrism-LvT-Large video+text fwd",
                  "lvt_base": "VideoPrism-LvT-Base video+text fwd"}[args.workload]
-        wl = (f"{name} bf16 forward, B={B} clips/GPU x {world} GPU, {T}x288x288x3"
+        wl = (f"{name} {args.dtype} forward, B={B} clips/GPU x {world} GPU, {T}x288x288x3"
               + (f", {args.queries} text queries x 64 tokens, gathered video_emb @ text_emb.T"
                  if lvt else "")
               + ((", gloo all-gather (stand-in)" if args.standin else
                   ", RCCL all-gather (vp_allgather) of pooled embeddings") if gather else ""))
         line = {
-            "metric": f"clips/sec (16x288x288) {label}; % MFMA peak",
+            "metric": f"clips/sec (16x288x288) {label}{' fp32' if args.dtype == 'f32' else ''}; % MFMA peak",
             "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic uniform[0,1) clips generated on device; random-init weights of the "
                     "real architecture (no checkpoint offline)",
             "config": {"workload": wl,
                        "model": name, "global_batch": B * world, "frames": T,
                        "parallelism": f"dp{world} (batch-sharded clips)"},
             "mfma_util_whole_forward": round((value / world * gpc + text_gf / ms_per_step * 1e3)
-                                             / 1e3 / PEAK_BF16_TFLOPS, 4),
+                                             / 1e3 / peak_tf, 4),
             "gflop_per_clip": round(gpc, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,
