@@ -136,9 +136,11 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 // so each lane owns 4 consecutive columns of one row for the 16-byte epilogue stores.  XCD-contiguous tile
 // ranges (workgroup b runs on XCD b % 8), M-block-major inside a range so an A block stays in its XCD's L2
 // across the N tiles.  Exact fp32 products summed in fp32 (another order than v1: k-pairs, then steps).
-// Measured (tools/gemm_f32_ab.py, Base B = 4 shapes, profiles/r06/fp32_gemm_ab.txt): 1-5 % faster than v1
-// (ffn2 593.7 vs 624.5 us); a K-tile of 32 (73.7 KB of LDS: two workgroups per CU) was 8-38 % slower.
-template <int EPI, int TK2 = 16>
+// Within a K-tile the second half's LDS reads are issued behind the first step's MFMAs (PIPE), so only four reads'
+// latency is exposed after each barrier.  Measured (tools/gemm_f32_ab.py, Base B = 4 shapes, profiles/r06/
+// fp32_gemm_ab.txt): 0-8 % faster than v1 (ffn2 577.4 vs 625.6 us, q|k|v 449.1 vs 474.8; without PIPE 603.0 / 467.4);
+// a K-tile of 32 (73.7 KB of LDS: two workgroups per CU) was 8-38 % slower.
+template <int EPI, int TK2 = 16, bool PIPE = true>
 __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict__ A, int64_t lda,
                                                         const float* __restrict__ W, int64_t ldw,
                                                         int M, int N, int K, EpiArgs ep) {
@@ -185,21 +187,38 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict_
     const int cur = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * TK2);
     f32x4 av[2][SH / 4], wv[2][SH / 4];  // [block][k SH h + 4 j .. + 3]
+    auto rd = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int j = 0; j < SH / 4; ++j) {
+      for (int b = 0; b < 2; ++b) {
         av[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][0][(wm * 64 + b * 32 + l32) * ROW2 + SH * half + 4 * j]);
         wv[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][1][(wn * 64 + b * 32 + l32) * ROW2 + SH * half + 4 * j]);
       }
-#pragma unroll
-    for (int st = 0; st < SH; ++st)
+    };
+    auto mm = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
           acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[nb][st >> 2][st & 3], av[mb][st >> 2][st & 3],
                                                              acc[nb][mb], 0, 0, 0);
+    };
+    if constexpr (PIPE && SH == 8) {
+      // the second half's reads issued behind the first step's MFMAs, so only 4 reads' latency is exposed
+      rd(0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(0);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(1); mm(2); mm(3);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(4); mm(5); mm(6); mm(7);
+    } else {
+#pragma unroll
+      for (int j = 0; j < SH / 4; ++j) rd(j);
+#pragma unroll
+      for (int st = 0; st < SH; ++st) mm(st);
+    }
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
