@@ -10,6 +10,10 @@ mkdir -p $O
 export TMPDIR=/tmp
 step() { local n=$1 t=$2; shift 2; echo "[$(date +%T)] $n start"; timeout -k 10 "$t" "$@"; local rc=$?; echo "[$(date +%T)] $n rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 test -f videoprism-mlx_amd/videoprism/libvideoprism_hip.so || { echo "product library missing"; exit 9; }
+# two gpurun calls (each within the 20-minute limit): PHASE 1 = tests, smoke, the Base bench and the rocprof runs;
+# PHASE 2 = the PMC traffic records and the benches that quote them
+PHASE=${1:-1}
+if [ "$PHASE" = 1 ]; then
 echo "[$(date +%T)] tests start"
 timeout -k 10 1000 bash -c "python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > $O/gputest.log 2>&1"
 rc=$?; echo "[$(date +%T)] tests rc=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
@@ -17,6 +21,8 @@ step smoke 300 bash -c "python -u -c 'import __graft_entry__ as g; g.smoke()' > 
 step bench_base 300 bash -c "python -u bench.py > $O/bench_base.log 2>&1"
 step rocprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof -o run -- python3 bench.py --no-cpu-baseline --no-peak
 step rocprof_lvt 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rocprof_lvt -o run -- python3 bench.py --workload lvt_large --no-peak
+exit 0
+fi
 step pmc_base 600 bash tools/pmc_traffic.sh $O/pmc_base base profiles/traffic_r06_base.json
 step pmc_large 600 bash tools/pmc_traffic.sh $O/pmc_large large profiles/traffic_r06_large.json
 step pmc_lvt 600 bash tools/pmc_traffic.sh $O/pmc_lvt lvt_large profiles/traffic_r06_lvt_large.json
