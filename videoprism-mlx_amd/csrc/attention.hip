@@ -603,19 +603,63 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(const float* __restrict__
 // fp32 (fprop_dtype=float32, the reference's default precision) on v_mfma_f32_32x32x2f32, any S: the
 // spatial attention (S = 256), other patch grids (S >= 128), long clips' temporal attention and the LvT
 // auxiliary encoder (S = T*N).  Exact fp32 products summed in fp32; the numerators exp(cap * tanh(x / cap))
-// with the same tanhf / expf as attn_f32_kernel.  With 0 < cap <= 50 every capped logit lies in [-cap, cap],
+// from capped_exp_f32x16 (a few fp32 ulp from exp(cap tanh(x / cap))).  With 0 < cap <= 50 every capped logit lies in [-cap, cap],
 // so the softmax needs no running max (the bf16 kernels' argument, vp_internal.h kMaxFastCap).
 // A workgroup owns 256 queries of one (sequence, head), 8 waves x 32 queries; K and V stream through LDS in
 // 128-key chunks, double-buffered (chunk c + 1's loads in flight in registers while chunk c is consumed; one
 // barrier per chunk), rows padded to 68 floats so the b128 K reads and the b64 V reads are conflict-free.
 // S^T = K.Q^T puts one query per lane column; the contraction index d is permuted per lane half
-// (d = 32 (l / 32) + step) so a lane's K operands are 32 consecutive floats of its key row.  O^T = V^T.P^T
+// (d = 32 (l / 32) + step) so a lane's K operands are 32 consecutive floats of its key row (numerators:
+// capped_exp_f32x16).  O^T = V^T.P^T
 // takes the numerators straight from the S^T accumulators: MFMA step r sums keys 8 (r / 4) + 4 (l / 32) + r % 4
 // -- the keys register r of each lane half holds -- and output row i of block b is d = 2 i + b, so a lane's
 // V operands are one 8-byte read.  Padded keys (MASK) weigh 0, a fully padded sequence gives uniform weights
 // (as attn_f32_kernel); TAIL (S % 256 != 0): query and key rows past S read row S - 1, keys past S weigh 0,
 // queries past S are not stored.
 // ------------------------------------------------------------------------------------
+// exp(cap * tanh(x / cap)) in fp32 for the 16 logits of a 32x32 tile (the MFMA kernel's numerators), accurate
+// to a few fp32 ulp without the libm calls (≈ 14 VALU operations and one transcendental per logit instead of ≈ 56):
+// cap tanh(x / cap) = x T(t^2), t = x / cap, with T(u) = tanh(sqrt u) / sqrt u fitted on u <= 0.55^2 by a
+// degree-5 polynomial (relative error 9.4e-10; 4.6e-8 evaluated in fp32); tiles holding a larger |t| take
+// tanh |t| = 1 - 2 / (e^{2|t|} + 1) there (no cancellation past 0.55: the result is >= 0.5; one Newton step on the
+// reciprocal).  The exponential keeps the rounding error of g log2e: exp(g) = 2^p (1 + ln2 (g log2e - p)), the
+// product's error recovered by an FMA against log2e split into fp32 hi + lo.  Emulated in fp32 against fp64 on
+// |x| <= 200, cap 50: max relative error 5.4e-6 (rms 1.3e-6) vs 4.1e-6 (1.2e-6) for fp32 tanhf / expf -- both set by
+// the fp32 rounding of cap tanh(.) itself, ~1.9e-6 of the exponent at 50.
+__device__ __forceinline__ void capped_exp_f32x16(const f32x16& x, float* e, float cap, float inv_cap) {
+  constexpr float c0 = 0.9999999990601012f, c1 = -0.33333310932806975f, c2 = 0.13332460381965514f,
+                  c3 = -0.05384268765140977f, c4 = 0.021039637749701284f, c5 = -0.00623554674883513f;
+  constexpr float kL = 1.4426950216293335f, kLlo = 1.92596298909109e-08f, kLn2 = 0.6931471805599453f;
+  float mx = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mx = fmaxf(mx, fabsf(x[i]));
+  const float xthr = 0.55f * cap, k2 = 2.0f * kL * inv_cap;
+  const bool big = __builtin_amdgcn_ballot_w64(mx >= xthr) != 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float t = x[i] * inv_cap;
+    const float u = t * t;
+    float P = fmaf(c5, u, c4);
+    P = fmaf(P, u, c3);
+    P = fmaf(P, u, c2);
+    P = fmaf(P, u, c1);
+    P = fmaf(P, u, c0);
+    float g = x[i] * P;
+    if (big) {
+      const float a2 = fminf(fabsf(x[i]) * k2, 64.0f);  // 2 |t| log2e, clamped: e^{44} already gives tanh = 1
+      const float d = __builtin_amdgcn_exp2f(a2) + 1.0f;
+      const float r0 = __builtin_amdgcn_rcpf(d);
+      const float r = fmaf(r0, fmaf(-d, r0, 1.0f), r0);
+      const float gl = copysignf(cap * fmaf(-2.0f, r, 1.0f), x[i]);
+      g = fabsf(x[i]) < xthr ? g : gl;
+    }
+    const float p = g * kL;
+    const float lo = fmaf(g, kLlo, fmaf(g, kL, -p));
+    const float E = __builtin_amdgcn_exp2f(p);
+    e[i] = fmaf(E, lo * kLn2, E);
+  }
+}
+
 constexpr int kF32Chunk = 128, kF32Row = 68;
 constexpr int kF32BufFloats = 2 * kF32Chunk * kF32Row + kF32Chunk;  // K, V, key paddings of one chunk
 constexpr int kF32MfmaLds = 2 * kF32BufFloats * 4 + 16;
@@ -685,6 +729,7 @@ __global__ __launch_bounds__(512) void attn_f32_mfma_kernel(const float* __restr
 
   f32x16 y0 = {}, y1 = {};  // O^T blocks b = 0 / 1: row i <-> d = 2 i + b
   float lsum = 0.0f;
+  const float inv_cap = 1.0f / cap;
   const int nch = (S + kF32Chunk - 1) / kF32Chunk;
   stage(0);
   store(0);
@@ -708,10 +753,12 @@ __global__ __launch_bounds__(512) void attn_f32_mfma_kernel(const float* __restr
         x = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qf[4 * i + 2], x, 0, 0, 0);
         x = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qf[4 * i + 3], x, 0, 0, 0);
       }
+      float ev[16];
+      capped_exp_f32x16(x, ev, cap, inv_cap);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int kl = kt * 32 + 8 * (r >> 2) + 4 * half + (r & 3);  // key within the chunk
-        float e = expf(cap * tanhf(x[r] / cap));
+        float e = ev[r];
         if constexpr (MASK) e = all_masked ? 1.0f : (kp[kl] != 0.0f ? 0.0f : e);
         if constexpr (TAIL) e = c * kF32Chunk + kl < S ? e : 0.0f;
         lsum += e;
