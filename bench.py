@@ -451,10 +451,12 @@ def _run(args, rank: int, local_rank: int, world: int, owned: list) -> None:
         avg_s = dom["ms"] / dom["launches"] / 1e3
         fp = _native.source_fingerprint()
         traffic, tsrc = None, None
+        # fp32 kernels have records of their own (tools/pmc_traffic.sh ... f32: workload label <workload>_f32)
+        tlabel = args.workload + ("_f32" if args.dtype == "f32" else "")
         for tpath in ([args.traffic] if args.traffic else
-                      sorted(glob.glob(os.path.join(ROOT, "profiles", f"traffic_r*_{args.workload}.json")),
+                      sorted(glob.glob(os.path.join(ROOT, "profiles", f"traffic_r*_{tlabel}.json")),
                              reverse=True)):
-            traffic, tsrc = load_traffic(tpath, dom_symbol, args.workload, fp)
+            traffic, tsrc = load_traffic(tpath, dom_symbol, tlabel, fp)
             if traffic is not None:
                 break
         if dom["flops"] > 0:

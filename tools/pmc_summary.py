@@ -56,7 +56,8 @@ if len(sys.argv) > 4 and sys.argv[2] == "--json":
                                  "videoprism-mlx_amd")]
     from videoprism import _native
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes over "
-                     f"`bench.py --workload {sys.argv[4]}` (tools/pmc_traffic.sh); hbm_bytes_per_launch "
+                     f"`bench.py --workload {sys.argv[4].removesuffix('_f32')}"
+                     f"{' --dtype f32' if sys.argv[4].endswith('_f32') else ''}` (tools/pmc_traffic.sh); hbm_bytes_per_launch "
                      "= 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section: FETCH_SIZE "
                      "reads half of wide streaming reads on gfx950; Infinity-Cache hits are counted)",
            "workload": sys.argv[4], "src_hash": _native.source_fingerprint(), "kernels": {}}
