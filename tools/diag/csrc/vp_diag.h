@@ -18,4 +18,9 @@ hipError_t gemm_bf16_w4_ffn2_abl(int abl, const bf16_t* A, const bf16_t* W, int 
 hipError_t gemm_bf16_w4_tattn_abl(int which, int abl, const bf16_t* A, const bf16_t* W, int M, int N, int K,
                                   const EpiArgs& ep, hipStream_t s);
 
+// fp32 GEMM variants (gemm_f32_var.hip): var 0 = the product schedule, 1 = mid-K-tile barrier; abl bits
+// 2 = no LDS reads, 4 = no staging, 8 = no epilogue, 16 = no barrier; epi EPI_BF16 / EPI_GELU_BF16 (fp32 out)
+hipError_t gemm_f32_var(int var, int abl, int epi, const float* A, const float* W, int M, int N, int K,
+                        const EpiArgs& ep, hipStream_t s);
+
 }  // namespace vp

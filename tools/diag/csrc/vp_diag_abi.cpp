@@ -60,4 +60,14 @@ int vp_dev_gemm_tattn_abl(int which, int abl, const void* A, const void* W, int6
   return VP_OK;
 }
 
+// fp32 GEMM variants (gemm_f32_var.hip): out [M][N] fp32 = A [M][K] . W [N][K]^T + bias (GELU for epi 1)
+int vp_dev_gemm_f32_var(int var, int abl, int epi, const float* A, const float* W, int64_t M, int64_t N, int64_t K,
+                        float* out, const float* bias, void* stream) {
+  using namespace vp;
+  EpiArgs ep;
+  ep.out = out; ep.ldo = N; ep.bias = bias;
+  VP_HIP(gemm_f32_var(var, abl, epi, A, W, (int)M, (int)N, (int)K, ep, static_cast<hipStream_t>(stream)));
+  return VP_OK;
+}
+
 }  // extern "C"

@@ -16,14 +16,18 @@ namespace {
 
 constexpr int TM = 128, TN = 128, TK = 16, LDSROW = 144;
 
-template <int EPI>
+// GFIT: the GELU as gelu_erfc_fit2 (v2 kernel) instead of the libm erff (v1 kernel)
+template <int EPI, bool GFIT = false>
 __device__ __forceinline__ void epi_f32(const EpiArgs& ep, int N, int m, int n, float v0, float v1,
                                         float v2, float v3) {
   float* out = static_cast<float*>(ep.out) + (int64_t)m * ep.ldo + n;
   if constexpr (EPI == EPI_BF16) {
     *reinterpret_cast<float4*>(out) = make_float4(v0, v1, v2, v3);
   } else if constexpr (EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
-    if constexpr (EPI == EPI_GELU_BF16) {
+    if constexpr (EPI == EPI_GELU_BF16 && GFIT) {
+      const f32x2_t g0 = gelu_erfc_fit2(f32x2_t{v0, v1}), g1 = gelu_erfc_fit2(f32x2_t{v2, v3});
+      v0 = g0.x; v1 = g0.y; v2 = g1.x; v3 = g1.y;
+    } else if constexpr (EPI == EPI_GELU_BF16) {
       v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
     } else {
       v0 = relu_nan(v0); v1 = relu_nan(v1); v2 = relu_nan(v2); v3 = relu_nan(v3);
@@ -130,68 +134,85 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 // Same 128x128 workgroup tile and 2x2 waves of 64x64, but on 32x32x2 MFMAs (2 x 2 blocks per wave, 32 MFMAs
 // per K-tile instead of 64) with operands read as whole 16-B runs: in K-tile step s (0..7) lane half h
 // contracts k = 8 h + s, so a lane's 8 operands of a K-tile are 8 consecutive floats of its row (two
-// ds_read_b128 per row) and the LDS tiles keep the global row-major layout ([row][16 k], rows padded to 20
-// floats: conflict-free b128 reads, plain float4 copies in, no transposition).  Operands swapped as in v1
-// (D^T = W.A^T): register r of block (nb, mb) is output row m = l % 32, column n = 8 (r / 4) + 4 (l / 32) + r % 4,
-// so each lane owns 4 consecutive columns of one row for the 16-byte epilogue stores.  XCD-contiguous tile
-// ranges (workgroup b runs on XCD b % 8), M-block-major inside a range so an A block stays in its XCD's L2
-// across the N tiles.  Exact fp32 products summed in fp32 (another order than v1: k-pairs, then steps).
-// Within a K-tile the second half's LDS reads are issued behind the first step's MFMAs (PIPE), so only four reads'
-// latency is exposed after each barrier.  Measured (tools/gemm_f32_ab.py, Base B = 4 shapes, profiles/r06/
-// fp32_gemm_ab.txt): 0-8 % faster than v1 (ffn2 577.4 vs 625.6 us, q|k|v 449.1 vs 474.8; without PIPE 603.0 / 467.4);
-// a K-tile of 32 (73.7 KB of LDS: two workgroups per CU) was 8-38 % slower.
-template <int EPI, int TK2 = 16, bool PIPE = true>
+// ds_read_b128 per row).  Operands swapped as in v1 (D^T = W.A^T): register r of block (nb, mb) is output row
+// m = l % 32, column n = 8 (r / 4) + 4 (l / 32) + r % 4, so each lane owns 4 consecutive columns of one row for
+// the 16-byte epilogue stores.  XCD-contiguous tile ranges (workgroup b runs on XCD b % 8), M-block-major
+// inside a range so an A block stays in its XCD's L2 across the N tiles.  Exact fp32 products summed in fp32
+// (another order than v1: k-pairs, then steps).  Within a K-tile the second half's LDS reads are issued behind
+// the first step's MFMAs, so only four reads' latency is exposed after each barrier.
+// Staging by LDS-DMA (buffer_load_dwordx4 ... lds: 16 B per lane straight into LDS, no staging registers and no
+// ds_write): each 1-KiB wave instruction fills 16 whole 64-B rows of a tile, so the tiles are unpadded
+// [row][4 chunks of 16 B] with chunk c of row r in slot c ^ ((r >> 2) & 3) -- the lane picks its source chunk,
+// and the operand reads undo the swizzle; conflict-free for the ds_read_b128 lane groups (MI355X_MICROARCH.md
+// §LDS: per group the 4 lanes of each row residue mod 4 sit in 4 distinct slots).  Measured (tools/
+// gemm_f32_var.py, Base B = 8 shapes, profiles/r06/fp32_gemm_var.txt): bitwise the register-staged kernel's
+// sums, 5-9 % faster (q|k|v 818 vs 883 us, post 278 vs 302, ffn2 1057 vs 1151).  The register-staged form
+// measured 0-8 % faster than v1 (profiles/r06/fp32_gemm_ab.txt); a K-tile of 32 (two workgroups per CU) was
+// 8-38 % slower.  Its GELU epilogue is gelu_erfc_fit2 (no libm branches; ffn_layer1 1157 vs 1228 us).
+template <int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict__ A, int64_t lda,
                                                         const float* __restrict__ W, int64_t ldw,
                                                         int M, int N, int K, EpiArgs ep) {
-  constexpr int ROW2 = TK2 + 4, SPR = TK2 / 4;  // row stride (floats), float4 per row
-  constexpr int NST = TM * SPR / 256;            // float4 of A (and of W) per thread per K-tile
-  constexpr int SH = TK2 / 2;                     // steps per K-tile (k = SH h + s)
-  __shared__ __attribute__((aligned(16))) float lds[2][2][TM * ROW2];  // [buffer][A | W][row][k]
+  constexpr int TK2 = 16;
+  __shared__ __attribute__((aligned(16))) float lds[2][2][TM * TK2];  // [buffer][A | W][row][16 k, swizzled]
+  typedef __attribute__((address_space(3))) void lds_void;
   const int tilesN = N / TN;
   int bid = (int)blockIdx.x;
   if (gridDim.x % 8 == 0) bid = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
   const int m0 = (bid / tilesN) * TM, n0 = (bid % tilesN) * TN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   const int wm = w >> 1, wn = w & 1;
   const int half = lane >> 5, l32 = lane & 31;
-  // staging: 128 rows x SPR float4 of A and of W per K-tile, NST of each per thread
-  f32x4 ra[NST], rw[NST];
-  auto gload = [&](int k0) __attribute__((always_inline)) {
+  // staging: wave w fills rows 32 w .. 32 w + 31 of A and of W (pieces 2 w, 2 w + 1 of 16 rows); lane i of a
+  // piece: row i / 4, slot i % 4 <- source chunk slot ^ swizzle.  The descriptors span the tile's 128 rows.
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)m0 * lda), 0, (int)(TM * lda * 4), 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)n0 * ldw), 0, (int)(TN * ldw * 4), 0x00020000);
+  uint32_t voA[2], voW[2];
 #pragma unroll
-    for (int i = 0; i < NST; ++i) {
-      const int idx = t + 256 * i, row = idx / SPR, c4 = (idx % SPR) * 4;
-      ra[i] = *reinterpret_cast<const f32x4*>(A + (int64_t)(m0 + row) * lda + k0 + c4);
-      rw[i] = *reinterpret_cast<const f32x4*>(W + (int64_t)(n0 + row) * ldw + k0 + c4);
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * (2 * wu + i) + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    voA[i] = (uint32_t)(r * lda * 4 + c * 16);
+    voW[i] = (uint32_t)(r * ldw * 4 + c * 16);
+  }
+  auto dma = [&](int buf, int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = 2 * wu + i;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_void*)&lds[buf][0][q * 256], 16, voA[i], k0 * 4, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, (lds_void*)&lds[buf][1][q * 256], 16, voW[i], k0 * 4, 0, 0);
     }
   };
-  auto sstore = [&](int buf) __attribute__((always_inline)) {
+  // operand reads: block b's row of this lane, chunk 2 h + j (k = 8 h + 4 j .. + 3), through the swizzle
+  int offA[2][2], offW[2][2];
 #pragma unroll
-    for (int i = 0; i < NST; ++i) {
-      const int idx = t + 256 * i, row = idx / SPR, c4 = (idx % SPR) * 4;
-      *reinterpret_cast<f32x4*>(&lds[buf][0][row * ROW2 + c4]) = ra[i];
-      *reinterpret_cast<f32x4*>(&lds[buf][1][row * ROW2 + c4]) = rw[i];
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ra = wm * 64 + b * 32 + l32, rw = wn * 64 + b * 32 + l32, c = 2 * half + j;
+      offA[b][j] = ra * TK2 + 4 * (c ^ ((ra >> 2) & 3));
+      offW[b][j] = rw * TK2 + 4 * (c ^ ((rw >> 2) & 3));
     }
-  };
   f32x16 acc[2][2];  // [n block][m block]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   const int nk = K / TK2;
-  gload(0);
-  sstore(0);
+  dma(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 #pragma unroll 1
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * TK2);
-    f32x4 av[2][SH / 4], wv[2][SH / 4];  // [block][k SH h + 4 j .. + 3]
+    if (kt + 1 < nk) dma(cur ^ 1, (kt + 1) * TK2);  // buffer cur ^ 1: every read of it was before the last barrier
+    f32x4 av[2][2], wv[2][2];  // [block][chunk j]
     auto rd = [&](int j) __attribute__((always_inline)) {
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        av[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][0][(wm * 64 + b * 32 + l32) * ROW2 + SH * half + 4 * j]);
-        wv[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][1][(wn * 64 + b * 32 + l32) * ROW2 + SH * half + 4 * j]);
+        av[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][0][offA[b][j]]);
+        wv[b][j] = *reinterpret_cast<const f32x4*>(&lds[cur][1][offW[b][j]]);
       }
     };
     auto mm = [&](int st) __attribute__((always_inline)) {
@@ -202,24 +223,18 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict_
           acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[nb][st >> 2][st & 3], av[mb][st >> 2][st & 3],
                                                              acc[nb][mb], 0, 0, 0);
     };
-    if constexpr (PIPE && SH == 8) {
-      // the second half's reads issued behind the first step's MFMAs, so only 4 reads' latency is exposed
-      rd(0);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(0);
-      __builtin_amdgcn_sched_barrier(0);
-      rd(1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(1); mm(2); mm(3);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(4); mm(5); mm(6); mm(7);
-    } else {
-#pragma unroll
-      for (int j = 0; j < SH / 4; ++j) rd(j);
-#pragma unroll
-      for (int st = 0; st < SH; ++st) mm(st);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
+    // the second half's reads issued behind the first step's MFMAs, so only 4 reads' latency is exposed
+    rd(0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(0);
+    __builtin_amdgcn_sched_barrier(0);
+    rd(1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(1); mm(2); mm(3);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(4); mm(5); mm(6); mm(7);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-tile has landed in LDS
     __syncthreads();
   }
 #pragma unroll
@@ -231,8 +246,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict_
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) {
         const f32x16& a = acc[nb][mb];
-        epi_f32<EPI>(ep, N, m0 + wm * 64 + mb * 32 + l32, n, a[4 * q] + b.x, a[4 * q + 1] + b.y,
-                     a[4 * q + 2] + b.z, a[4 * q + 3] + b.w);
+        epi_f32<EPI, true>(ep, N, m0 + wm * 64 + mb * 32 + l32, n, a[4 * q] + b.x, a[4 * q + 1] + b.y,
+                           a[4 * q + 2] + b.z, a[4 * q + 3] + b.w);
       }
     }
 }
@@ -254,11 +269,14 @@ hipError_t launch(const float* A, int64_t lda, const float* W, int64_t ldw, int 
 
 }  // namespace
 
-const char* gemm_f32_check(int M, int N, int K) {
+const char* gemm_f32_check(int M, int N, int K, int64_t lda, int64_t ldw) {
   if (M <= 0 || N <= 0 || K <= 0) return "gemm_f32: non-positive dimension";
   if (M % TM) return "gemm_f32: M must be a multiple of 128";
   if (N % TN) return "gemm_f32: N must be a multiple of 128";
   if (K % TK) return "gemm_f32: K must be a multiple of 16";
+  // the v2 kernel's LDS-DMA descriptors span 128 rows of A / W in bytes (int32) with 16-B row starts
+  if (lda < K || ldw < K || lda % 4 || ldw % 4) return "gemm_f32: lda, ldw must be >= K and multiples of 4";
+  if ((int64_t)TM * lda * 4 > 0x7fffffff || (int64_t)TN * ldw * 4 > 0x7fffffff) return "gemm_f32: lda, ldw too large";
   return nullptr;
 }
 

@@ -318,7 +318,7 @@ int forward_chunk(vp_handle* h, const void* video, int in_dtype, int64_t B, int6
   f.pf = &h->prof;
   float* ln_rs = f.ln_rs;
   const int epi_pos = bf ? EPI_POS_BF16 : EPI_POS_F32;
-  const char* ge = bf ? gemm_bf16_check(Mp, 3 * D, D, D, D) : gemm_f32_check(Mp, 3 * D, D);
+  const char* ge = bf ? gemm_bf16_check(Mp, 3 * D, D, D, D) : gemm_f32_check(Mp, 3 * D, D, D, D);
   if (ge) return fail(VP_ENOTSUP, ge);
   const double dM = M, dD = D, dE = (double)es;
   auto gbytes = [&](double K, double N, double outb, double resid) {  // algorithmic GEMM bytes
@@ -507,7 +507,7 @@ int vp_op_gemm(int precision, int epilogue, const void* A, int64_t lda, const vo
     if (e) return fail(VP_EINVAL, e);
     VP_HIP(gemm_bf16_auto(epilogue, (const bf16_t*)A, lda, (const bf16_t*)W, ldw, (int)M, (int)N, (int)K, ep, s));
   } else if (precision == VP_F32) {
-    const char* e = gemm_f32_check((int)M, (int)N, (int)K);
+    const char* e = gemm_f32_check((int)M, (int)N, (int)K, lda, ldw);
     if (e) return fail(VP_EINVAL, e);
     VP_HIP(gemm_f32(epilogue, (const float*)A, lda, (const float*)W, ldw, (int)M, (int)N, (int)K, ep, s));
   } else {
@@ -522,7 +522,7 @@ int vp_dev_gemm_kernel(int which, int epi, const void* A, const void* W, int64_t
                        int64_t K, void* out, const float* bias, const void* resid, const float* pos,
                        int64_t pos_rows, const float* rowpad, void* stream) {
   using namespace vp;
-  const char* e = which == 1 ? nullptr : (which == 32 || which == 33) ? gemm_f32_check((int)M, (int)N, (int)K)
+  const char* e = which == 1 ? nullptr : (which == 32 || which == 33) ? gemm_f32_check((int)M, (int)N, (int)K, K, K)
                                                                        : gemm_bf16_check((int)M, (int)N, (int)K, K, K);
   if (e) return fail(VP_EINVAL, e);
   EpiArgs ep;

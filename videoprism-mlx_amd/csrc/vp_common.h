@@ -42,6 +42,35 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
 
+// Exact-erf GELU without the libm call, on a pair of values (the fp32 GEMM's epilogue): erfc(|z|) =
+// t exp(-z^2 + P(t)), t = 1 / (1 + |z| / 2), P of degree 9 (the Chebyshev fit of Numerical Recipes' erfcc,
+// relative error <= 1.2e-7), one Newton step on the reciprocal; Phi(x) = 1 - erfc / 2 (x >= 0) or erfc / 2.
+// Branch-free (libm's erff runs several branches per wave), two transcendentals per value, the polynomial on
+// packed FMAs.  Error vs fp64 on [-12, 12] (emulated, tools/gelu_erfc_accuracy.py): max 2.3e-7 / mean 5.9e-8 on
+// [1, 4), the same band as a correctly rounded fp32 erf's (2.9e-7 / 6.6e-8); at the ffn_layer1 GEMM 5.19e-6 max /
+// 1.950e-7 mean vs the libm form's 5.14e-6 / 1.943e-7 (profiles/r06/fp32_gemm_var.txt).
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2_t gelu_erfc_fit2(f32x2_t x) {
+  const f32x2_t za = __builtin_elementwise_abs(x) * f32x2_t(0.70710678118654752f);
+  const f32x2_t d = __builtin_elementwise_fma(f32x2_t(0.5f), za, f32x2_t(1.0f));
+  f32x2_t t = f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  t = __builtin_elementwise_fma(t, __builtin_elementwise_fma(-d, t, f32x2_t(1.0f)), t);
+  f32x2_t p = f32x2_t(0.17087277f);
+  p = __builtin_elementwise_fma(p, t, f32x2_t(-0.82215223f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(1.48851587f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(-1.13520398f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(0.27886807f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(-0.18628806f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(0.09678418f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(0.37409196f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(1.00002368f));
+  p = __builtin_elementwise_fma(p, t, f32x2_t(-1.26551223f));
+  const f32x2_t y = __builtin_elementwise_fma(-za, za, p) * f32x2_t(1.4426950408889634f);
+  const f32x2_t hec = f32x2_t(0.5f) * t * f32x2_t{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+  const f32x2_t phi = f32x2_t{x.x >= 0.0f ? 1.0f - hec.x : hec.x, x.y >= 0.0f ? 1.0f - hec.y : hec.y};
+  return x * phi;
+}
+
 // nontemporal (streaming) stores of 8 / 16 bytes: outputs that the next kernel reads back from
 // HBM anyway go past L2 instead of being written back from it later
 typedef unsigned nt_u32x2 __attribute__((ext_vector_type(2)));

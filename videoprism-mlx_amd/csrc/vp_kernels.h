@@ -122,7 +122,7 @@ hipError_t gemm_bf16_auto(int epi, const bf16_t* A, int64_t lda, const bf16_t* W
                           int N, int K, const EpiArgs& ep, hipStream_t s);
 
 // ---- fp32 GEMM for fprop_dtype=float32 (gemm_f32.hip) ----
-const char* gemm_f32_check(int M, int N, int K);
+const char* gemm_f32_check(int M, int N, int K, int64_t lda, int64_t ldw);
 // version 2 (default): the 32x32x2 kernel; 1: round 1's 16x16x4 kernel (A/B through vp_dev_gemm_kernel)
 hipError_t gemm_f32(int epi, const float* A, int64_t lda, const float* W, int64_t ldw, int M,
                     int N, int K, const EpiArgs& ep, hipStream_t s, int version = 2);

@@ -148,6 +148,8 @@ _SIGNATURES = {
 }
 # diag library only (ablation builds for tools/)
 _DIAG_SIGNATURES = {
+    "vp_dev_gemm_f32_var": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_void_p,
+                                    c_void_p, c_void_p]),
     "vp_dev_attention_long_var": (c_int, [c_int, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_float, c_void_p]),
     "vp_dev_gemm_tattn_abl": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p,
                                       c_void_p, c_void_p, c_void_p, c_int64, c_float, c_void_p]),
