@@ -726,3 +726,26 @@ def test_gemm_f32_kernels(cuda, M, N, K, epi):
         torch.cuda.synchronize()
         err = float((o.double() - ref).abs().max())
         assert err < 2e-5, (which, err)
+
+
+@pytest.mark.parametrize("M,N,K,pad_a,pad_w", [(384, 256, 80, 12, 4), (256, 384, 768, 4, 36), (128, 128, 16, 0, 8)])
+def test_gemm_f32_strided_operands(cuda, M, N, K, pad_a, pad_w):
+    """The fp32 GEMM's LDS-DMA staging addresses A / W rows through lda / ldw (buffer descriptors over the tile's
+    128 rows): row-strided operands (views of wider tensors, odd K-tile counts) against fp64, and the row
+    strides it cannot stage (not a multiple of 4 floats, below K) refused with VP_EINVAL before any launch."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    A = torch.randn(M, K + pad_a, generator=g).to(cuda)
+    Wt = (torch.randn(N, K + pad_w, generator=g) / K ** 0.5).to(cuda)
+    b = (torch.randn(N, generator=g) * 0.1).to(cuda)
+    a, w = A[:, :K], Wt[:, :K]
+    assert a.stride(0) == K + pad_a and w.stride(0) == K + pad_w
+    y = a.double() @ w.double().T + b.double()
+    for epi in (nat.EPI_STORE, nat.EPI_GELU):
+        out = nat.op_gemm(a, w, b, epi)
+        torch.cuda.synchronize()
+        ref = 0.5 * y * (1 + torch.erf(y / 2 ** 0.5)) if epi == nat.EPI_GELU else y
+        err = float((out.double() - ref).abs().max())
+        assert err < 2e-5, (epi, err)
+    bad = torch.randn(M, K + 1, generator=g).to(cuda)[:, :K]  # lda = K + 1: rows not 16-B aligned
+    with pytest.raises(ValueError, match="lda"):
+        nat.op_gemm(bad, w, b, nat.EPI_STORE)
