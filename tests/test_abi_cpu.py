@@ -100,3 +100,15 @@ def test_null_arguments_are_einval():
     assert lib.vp_finalize(None) == _native.VP_EINVAL
     assert lib.vp_forward(None, None, 0, 1, 1, 18, 18, None, None, 0, None, None, 0, None) == _native.VP_EINVAL
     assert lib.vp_op_attention(_native.VP_BF16, None, None, 1, 256, 12, 50.0, None, None) == _native.VP_EINVAL
+
+
+def test_kernel_short_name_keys():
+    """bench.py keys PMC traffic records (tools/pmc_summary.py) by the short kernel symbol: template names
+    with a suffix after `_kernel` (gemm_f32_kernel2) keep their template arguments like the others."""
+    from videoprism import _native
+    assert _native.kernel_short_name("void vp::(anonymous namespace)::gemm_f32_kernel2<1>(float const*, long)") == \
+        "gemm_f32_kernel2<1>"
+    assert _native.kernel_short_name("void vp::(anonymous namespace)::gemm_bf16_w4_kernel<16, true, false, 0, false>"
+                                     "(unsigned short const*)") == "gemm_bf16_w4_kernel<16, true, false, 0, false>"
+    assert _native.kernel_short_name("void vp::(anonymous namespace)::layernorm_kernel(float const*)") == \
+        "layernorm_kernel"

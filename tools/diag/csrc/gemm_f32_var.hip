@@ -9,7 +9,8 @@
 //   barrier, behind steps 4-7 (one barrier per K-tile still; every LDS read latency hidden behind MFMAs);
 //   VAR 2 = the product schedule with the staging loads issued two K-tiles ahead (two register sets);
 //   VAR 3 = the product schedule with LDS-DMA staging into swizzled unpadded tiles; VAR 5 / 6 = its persistent
-//   form (gemm_f32_pers_kernel), 6 with a staggered start.
+//   form (gemm_f32_pers_kernel), 6 with a staggered start; VAR 7 = VAR 3 (+ packed GELU) in an N-grouped tile order
+//   (abl = N-tiles per group).
 // Epilogues: EPI_BF16 (fp32 store + bias) and EPI_GELU_BF16 (erf GELU), as the product's epi_f32.
 #include "vp_common.h"
 #include "vp_diag.h"
@@ -57,7 +58,15 @@ __global__ __launch_bounds__(256) void gemm_f32_var_kernel(const float* __restri
   const int tilesN = N / VTN;
   int bid = (int)blockIdx.x;
   if (gridDim.x % 8 == 0) bid = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
-  const int m0 = (bid / tilesN) * VTM, n0 = (bid % tilesN) * VTN;
+  int m0 = (bid / tilesN) * VTM, n0 = (bid % tilesN) * VTN;
+  if constexpr (VAR == 7) {
+    // N-grouped order (ngrp = ep.ldr N-tiles, host: tilesN % ngrp == 0, M / 128 % 8 == 0): each XCD sweeps its
+    // M-blocks once per group of ngrp N-tiles, so the group's W rows stay in the XCD's L2
+    const int ngrp = (int)ep.ldr, mbx = (M / VTM) >> 3, x = bid / (mbx * tilesN), u = bid - x * mbx * tilesN;
+    const int gi = u / (mbx * ngrp), r = u - gi * mbx * ngrp, rm = r / ngrp;
+    m0 = (x * mbx + rm) * VTM;
+    n0 = (gi * ngrp + (r - rm * ngrp)) * VTN;
+  }
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int half = lane >> 5, l32 = lane & 31;
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(256) void gemm_f32_var_kernel(const float* __restri
       body(kt, std::integral_constant<int, 0>{});
       body(kt + 1, std::integral_constant<int, 1>{});
     }
-  } else if constexpr (VAR == 3) {
+  } else if constexpr (VAR == 3 || VAR == 7) {
     // LDS-DMA staging (buffer_load ... lds, 16 B per lane): no staging registers and no ds_write.  Tiles
     // unpadded, [row][4 chunks of 16 B] (64-B rows), chunk c of row r stored in slot c ^ ((r >> 2) & 3):
     // conflict-free for the operand reads' ds_read_b128 lane groups (MI355X_MICROARCH.md §LDS).  Wave w
@@ -459,6 +468,14 @@ hipError_t gemm_f32_var(int var, int abl, int epi, const float* A, const float* 
       hipLaunchKernelGGL((gemm_f32_pers_kernel<EPI_GELU_BF16>), dim3(G), dim3(256), 0, s, A, (int64_t)K, W, (int64_t)K,
                          M, N, K, ep, st);
     return hipGetLastError();
+  }
+  if (var == 7) {  // VAR 3 in N-grouped tile order, abl = ngrp
+    const int tilesN = N / VTN;
+    if (abl < 1 || tilesN % abl || (M / VTM) % 8) return hipErrorInvalidValue;
+    EpiArgs e2 = ep;
+    e2.ldr = abl;
+    return epi == EPI_BF16 ? launch_var<EPI_BF16, 64, 7>(A, W, M, N, K, e2, s)
+                           : launch_var<EPI_GELU_BF16, 64, 7>(A, W, M, N, K, e2, s);
   }
   if (var == 3)
     return epi == EPI_BF16 ? by_abl<EPI_BF16, 3>(abl, A, W, M, N, K, ep, s)

@@ -13,7 +13,7 @@ import torch  # noqa: E402
 
 from videoprism import _native as nat  # noqa: E402
 
-CASES = [(0, 0), (3, 0), (3, 64), (5, 0), (6, 4), (6, 14), (3, 8)]
+CASES = [(0, 0), (3, 64), (7, 2), (7, 3), (7, 6)]
 
 
 def timeit(fn, iters=10, warm=2):
@@ -55,7 +55,7 @@ def main(B=8):
             f()
         torch.cuda.synchronize()
         same = {c: bool(torch.equal(outs[c], prod)) for c in CASES if c[1] == 0 and c[0] < 5}
-        ref_pers = outs[(3, 64)] if gelu else prod  # the persistent kernels use the packed libm-free GELU
+        ref_pers = outs[(3, 64)] if gelu else prod  # the persistent / reordered kernels use the packed GELU
         for c in CASES:
             if c[0] >= 5:
                 same[c] = bool(torch.equal(outs[c], ref_pers))

@@ -10,7 +10,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(\w+_kernel)<([^>]*)>", name)
+    m = re.search(r"(\w+_kernel\w*)<([^>]*)>", name)
     if "Cijk" in name:
         return "hipblaslt:" + name.split("_")[-2]
     if m:

@@ -450,10 +450,10 @@ def kernel_short_name(symbol: str) -> str:
     """'void vp::(anonymous namespace)::gemm_bf16_w4_kernel<9, 512, 0>(...)' ->
     'gemm_bf16_w4_kernel<9, 512, 0>' (the same key tools/pmc_summary.py gives rocprof's names)."""
     import re
-    m = re.search(r"(\w+_kernel)<([^>]*)>", symbol)
+    m = re.search(r"(\w+_kernel\w*)<([^>]*)>", symbol)
     if m:
         return f"{m.group(1)}<{m.group(2)}>"
-    m = re.search(r"(\w+_kernel)\b", symbol)
+    m = re.search(r"(\w+_kernel\w*)\b", symbol)
     return m.group(1) if m else symbol
 
 
