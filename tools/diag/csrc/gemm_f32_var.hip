@@ -10,7 +10,7 @@
 //   VAR 2 = the product schedule with the staging loads issued two K-tiles ahead (two register sets);
 //   VAR 3 = the product schedule with LDS-DMA staging into swizzled unpadded tiles; VAR 5 / 6 = its persistent
 //   form (gemm_f32_pers_kernel), 6 with a staggered start; VAR 7 = VAR 3 (+ packed GELU) in an N-grouped tile order
-//   (abl = N-tiles per group).
+//   (abl = N-tiles per group); VAR 8 = VAR 3 + packed GELU with full-row stores through LDS; VAR 9 = VAR 8 N-grouped.
 // Epilogues: EPI_BF16 (fp32 store + bias) and EPI_GELU_BF16 (erf GELU), as the product's epi_f32.
 #include "vp_common.h"
 #include "vp_diag.h"
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void gemm_f32_var_kernel(const float* __restri
   int bid = (int)blockIdx.x;
   if (gridDim.x % 8 == 0) bid = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
   int m0 = (bid / tilesN) * VTM, n0 = (bid % tilesN) * VTN;
-  if constexpr (VAR == 7) {
+  if constexpr (VAR == 7 || VAR == 9) {
     // N-grouped order (ngrp = ep.ldr N-tiles, host: tilesN % ngrp == 0, M / 128 % 8 == 0): each XCD sweeps its
     // M-blocks once per group of ngrp N-tiles, so the group's W rows stay in the XCD's L2
     const int ngrp = (int)ep.ldr, mbx = (M / VTM) >> 3, x = bid / (mbx * tilesN), u = bid - x * mbx * tilesN;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void gemm_f32_var_kernel(const float* __restri
       body(kt, std::integral_constant<int, 0>{});
       body(kt + 1, std::integral_constant<int, 1>{});
     }
-  } else if constexpr (VAR == 3 || VAR == 7) {
+  } else if constexpr (VAR == 3 || VAR == 7 || VAR == 8 || VAR == 9) {
     // LDS-DMA staging (buffer_load ... lds, 16 B per lane): no staging registers and no ds_write.  Tiles
     // unpadded, [row][4 chunks of 16 B] (64-B rows), chunk c of row r stored in slot c ^ ((r >> 2) & 3):
     // conflict-free for the operand reads' ds_read_b128 lane groups (MI355X_MICROARCH.md §LDS).  Wave w
@@ -264,6 +264,44 @@ __global__ __launch_bounds__(256) void gemm_f32_var_kernel(const float* __restri
   }
   if constexpr (ABL & 8) {
     if (ep.ldo != -12345) return;
+  }
+  if constexpr (VAR == 8 || VAR == 9) {
+    // full-row stores: each 32-row x 64-column block goes through the wave's 8 KiB of LDS (free: the last K-tile's
+    // barrier is behind every operand read) so that 16 lanes hold one row's 64 consecutive columns (256 B) per
+    // store instruction instead of 2 lanes holding 32 B.  16-B chunk c of LDS row r at chunk c ^ (r & 7).
+    float* stg = &lds[0][0][0] + w * 2048;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = nb * 8 + 2 * q + half;
+          const f32x16& a = acc[nb][mb];
+          *reinterpret_cast<f32x4*>(stg + l32 * 64 + 4 * (c ^ (l32 & 7))) =
+              f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
+        }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's block is in LDS (wave-private region)
+      __builtin_amdgcn_wave_barrier();
+      const int c = lane & 15;
+      const int n = n0 + wn * 64 + 4 * c;
+      const float4 b = *reinterpret_cast<const float4*>(ep.bias + n);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = 4 * i + (lane >> 4);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * 64 + 4 * (c ^ (r & 7)));
+        float v0 = v[0] + b.x, v1 = v[1] + b.y, v2 = v[2] + b.z, v3 = v[3] + b.w;
+        if constexpr (EPI == EPI_GELU_BF16) {
+          const vf2 g0 = gelu_erfc_fit2(vf2{v0, v1}), g1 = gelu_erfc_fit2(vf2{v2, v3});
+          v0 = g0.x; v1 = g0.y; v2 = g1.x; v3 = g1.y;
+        }
+        float* out = static_cast<float*>(ep.out) + (int64_t)(m0 + wm * 64 + mb * 32 + r) * ep.ldo + n;
+        *reinterpret_cast<float4*>(out) = make_float4(v0, v1, v2, v3);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();  // the reads of this block are done before the next block's writes
+    }
+    return;
   }
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb)
@@ -468,6 +506,17 @@ hipError_t gemm_f32_var(int var, int abl, int epi, const float* A, const float* 
       hipLaunchKernelGGL((gemm_f32_pers_kernel<EPI_GELU_BF16>), dim3(G), dim3(256), 0, s, A, (int64_t)K, W, (int64_t)K,
                          M, N, K, ep, st);
     return hipGetLastError();
+  }
+  if (var == 8)  // VAR 3 (+ packed GELU) with full-row stores through LDS
+    return epi == EPI_BF16 ? launch_var<EPI_BF16, 64, 8>(A, W, M, N, K, ep, s)
+                           : launch_var<EPI_GELU_BF16, 64, 8>(A, W, M, N, K, ep, s);
+  if (var == 9) {  // VAR 8 in N-grouped tile order, abl = ngrp
+    const int tilesN = N / VTN;
+    if (abl < 1 || tilesN % abl || (M / VTM) % 8) return hipErrorInvalidValue;
+    EpiArgs e2 = ep;
+    e2.ldr = abl;
+    return epi == EPI_BF16 ? launch_var<EPI_BF16, 64, 9>(A, W, M, N, K, e2, s)
+                           : launch_var<EPI_GELU_BF16, 64, 9>(A, W, M, N, K, e2, s);
   }
   if (var == 7) {  // VAR 3 in N-grouped tile order, abl = ngrp
     const int tilesN = N / VTN;

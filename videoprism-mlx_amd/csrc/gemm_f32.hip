@@ -152,14 +152,22 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict__ A, int64_t lda,
                                                         const float* __restrict__ W, int64_t ldw,
-                                                        int M, int N, int K, EpiArgs ep) {
+                                                        int M, int N, int K, int ngrp, EpiArgs ep) {
   constexpr int TK2 = 16;
   __shared__ __attribute__((aligned(16))) float lds[2][2][TM * TK2];  // [buffer][A | W][row][16 k, swizzled]
   typedef __attribute__((address_space(3))) void lds_void;
   const int tilesN = N / TN;
   int bid = (int)blockIdx.x;
   if (gridDim.x % 8 == 0) bid = (bid & 7) * ((int)gridDim.x >> 3) + (bid >> 3);
-  const int m0 = (bid / tilesN) * TM, n0 = (bid % tilesN) * TN;
+  int m0 = (bid / tilesN) * TM, n0 = (bid % tilesN) * TN;
+  if (ngrp != tilesN) {
+    // N-grouped order (host f32_ngrp: every XCD owns M / 1024 whole M-blocks): the XCD sweeps its M-blocks once
+    // per group of ngrp N-tiles, so the group's W rows stay in its L2 instead of W being re-fetched per M-block
+    const int mbx = (M / TM) >> 3, x = bid / (mbx * tilesN), u = bid - x * mbx * tilesN;
+    const int gi = u / (mbx * ngrp), r = u - gi * mbx * ngrp, rm = r / ngrp;
+    m0 = (x * mbx + rm) * TM;
+    n0 = (gi * ngrp + (r - rm * ngrp)) * TN;
+  }
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wu = __builtin_amdgcn_readfirstlane(w);
   const int wm = w >> 1, wn = w & 1;
@@ -237,19 +245,51 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel2(const float* __restrict_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-tile has landed in LDS
     __syncthreads();
   }
+  // epilogue through the wave's 8 KiB of LDS (free: every operand read is behind the last barrier): a 32-row x
+  // 64-column block is written from the accumulator layout (a lane: 16 columns of one row in 16-B pieces) and read
+  // back as 16 lanes per row of 64 consecutive columns, so each store / residual load instruction covers 4 rows x
+  // 256 B -- whole lines instead of 32 rows x 32 B (ffn_layer1: 1.74x the output bytes written at the HBM side
+  // before, 1.00x after).  16-B chunk c of row r sits at chunk c ^ (r & 7): conflict-free for the ds_write_b128
+  // lane groups.  Same values and epilogue arithmetic as storing from the accumulators.
+  float* stg = &lds[0][0][0] + w * 2048;
+  const int c16 = lane & 15;
+  const int n = n0 + wn * 64 + 4 * c16;
+  const float4 b = *reinterpret_cast<const float4*>(ep.bias + n);
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
+  for (int mb = 0; mb < 2; ++mb) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int n = n0 + wn * 64 + nb * 32 + 8 * q + 4 * half;
-      const float4 b = *reinterpret_cast<const float4*>(ep.bias + n);
+    for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-      for (int mb = 0; mb < 2; ++mb) {
+      for (int q = 0; q < 4; ++q) {
+        const int c = nb * 8 + 2 * q + half;
         const f32x16& a = acc[nb][mb];
-        epi_f32<EPI, true>(ep, N, m0 + wm * 64 + mb * 32 + l32, n, a[4 * q] + b.x, a[4 * q + 1] + b.y,
-                           a[4 * q + 2] + b.z, a[4 * q + 3] + b.w);
+        *reinterpret_cast<f32x4*>(stg + l32 * 64 + 4 * (c ^ (l32 & 7))) =
+            f32x4{a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]};
       }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the block is in LDS (a wave-private region)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 4 * i + (lane >> 4);
+      const f32x4 v = *reinterpret_cast<const f32x4*>(stg + r * 64 + 4 * (c16 ^ (r & 7)));
+      epi_f32<EPI, true>(ep, N, m0 + wm * 64 + mb * 32 + r, n, v[0] + b.x, v[1] + b.y, v[2] + b.z, v[3] + b.w);
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();  // this block's reads are done before the next block's writes
+  }
+}
+
+// N-tile group size of the fp32 GEMM's tile order (kernel2): the whole W when it fits the XCD's L2 share
+// (<= 3 MB) or when A is the stream that matters (K >= 2048: a group sweep would re-read A per group); else
+// groups whose W rows take <= 2.5 MB (Base q|k|v and ffn_layer1: 6 N-tiles).  ffn_layer1 at B = 8: fetched
+// bytes 1.86 -> 0.80 GB per launch, 5 % faster with the whole-line epilogue (profiles/r06/fp32_gemm_var.txt).
+int f32_ngrp(int M, int N, int K) {
+  const int tilesN = N / TN;
+  const int64_t w_tile = (int64_t)TN * K * 4;
+  if ((int64_t)tilesN * w_tile <= (3ll << 20) || K >= 2048 || (M / TM) % 8 || ((M / TM) * tilesN) % 8) return tilesN;
+  for (int d = tilesN; d >= 1; --d)
+    if (tilesN % d == 0 && (int64_t)d * w_tile <= (5ll << 19)) return d;
+  return tilesN;
 }
 
 template <int EPI>
@@ -261,8 +301,12 @@ hipError_t launch(const float* A, int64_t lda, const float* W, int64_t ldw, int 
                        ldw, M, N, K, ep);
   } else {
     VP_NOTE_KERNEL(gemm_f32_kernel2<EPI>);
-    hipLaunchKernelGGL(gemm_f32_kernel2<EPI>, dim3((M / TM) * (N / TN)), dim3(256), 0, s, A, lda, W,
-                       ldw, M, N, K, ep);
+    // 4 workgroups per CU fit (48-59 VGPRs, 32 KiB of LDS); at K >= 2048 (ffn_layer2, A streamed from HBM) 3 run
+    // faster (1106 vs 1170 us at B = 8, same box; the K = 768 launches equal or faster at 4: q|k|v 833 vs 843):
+    // 20 KiB of unused dynamic LDS caps them at 3
+    const size_t cap3 = K >= 2048 ? 20480 : 0;
+    hipLaunchKernelGGL(gemm_f32_kernel2<EPI>, dim3((M / TM) * (N / TN)), dim3(256), cap3, s, A, lda, W,
+                       ldw, M, N, K, f32_ngrp(M, N, K), ep);
   }
   return hipGetLastError();
 }
